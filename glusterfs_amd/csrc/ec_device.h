@@ -1,0 +1,95 @@
+/*
+ * ec_device.h -- internal boundary between the C host layer (ec_method.c) and
+ * the HIP device layer (ec_device.hip, ec_kernels.hip).  C-compatible; no HIP
+ * types leak into the C side (streams are opaque void pointers).
+ */
+#ifndef EC_MI355X_DEVICE_H
+#define EC_MI355X_DEVICE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECD_CHUNK 512u      /* EC_METHOD_CHUNK_SIZE (ec-method.h:29) */
+#define ECD_MAX_K 16u       /* EC_METHOD_MAX_FRAGMENTS (ec-method.h:23) */
+#define ECD_MAX_ROWS 32u    /* >= EC_MAX_NODES (31, ec.h:27-32) */
+#define ECD_MAX_PAT_BYTES 2048u
+
+/* One launch of the generic GF(2^8) combination kernel:
+ *   for every stripe t < nstripes and row r < rows:
+ *     out_base[r] + t*out_stride = XOR_p coef[r][p] * (in_base[src[p]] + t*in_stride)
+ * on 512-byte bit-sliced chunks.  A "pattern" is the packed byte string
+ * {src[k], coef[rows][k]}; with group_pattern != NULL, stripe t uses pattern
+ * group_pattern[t >> group_shift] (mixed per-stripe-range erasure patterns),
+ * otherwise pattern 0. */
+typedef struct ecd_combine_desc {
+    uint32_t k;             /* inputs per stripe (kernel template parameter) */
+    uint32_t rows;          /* output rows per stripe                        */
+    uint64_t nstripes;
+    uint64_t in_stride;     /* bytes between consecutive stripes of an input */
+    uint64_t out_stride;    /* bytes between consecutive stripes of a row    */
+    const void *in_base[ECD_MAX_ROWS];
+    void *out_base[ECD_MAX_ROWS];
+    const uint8_t *group_pattern; /* device array, or NULL                   */
+    uint32_t group_shift;         /* log2(stripes per pattern group), >= 3   */
+    uint32_t npatterns;
+    uint32_t pat_bytes;           /* bytes per packed pattern = k + rows*k   */
+    uint32_t pad;
+    uint8_t pat[ECD_MAX_PAT_BYTES];
+} ecd_combine_desc_t;
+
+/* Number of usable gfx950 devices (0 when none: callers fail, there is no
+ * CPU fallback anywhere in the product path). */
+int ecd_device_count(void);
+const char *ecd_last_error(void);
+
+/* ---- device-pointer entry points: asynchronous on `stream` (NULL = the
+ * calling thread's per-thread default stream of `device`); 0 or -errno. */
+
+/* Compile-time specialised Vandermonde encode (k+r in the shipped table). */
+int ecd_has_vander(uint32_t k, uint32_t n);
+int ecd_encode_vander(int device, void *stream, uint32_t k, uint32_t n,
+                      uint64_t nstripes, const void *in, void *const *out);
+/* Generic combination (decode, mixed decode, generic encode, heal). */
+int ecd_combine(int device, void *stream, const ecd_combine_desc_t *d);
+int ecd_sync(int device, void *stream);
+
+/* ---- host-memory entry points: stripes are partitioned across `ndev`
+ * devices (0 = all visible), each device moves its range over PCIe with
+ * pinned staging and overlapped H2D / compute / D2H, and the call blocks.
+ * Buffers may be pageable or pinned host memory. */
+
+/* Encode: in = nstripes*k*512 bytes, out[i] = nstripes*512 bytes.  enc_pat
+ * (k + n*k bytes, direct coefficients) is used when no specialised encoder
+ * exists for k+n. */
+int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes,
+                    const void *in, void *const *out, const uint8_t *enc_pat);
+
+/* Decode / reconstruct: frags[0..nfrags) are fragment buffers of
+ * nstripes*512 bytes (NULL for fragments no pattern reads).  Output: when
+ * outs is NULL, out = nstripes*rows*512 bytes, stripe-major (decoded data);
+ * otherwise outs[r] = nstripes*512 bytes per row (regenerated fragments).  pats
+ * holds npatterns packed patterns of k + rows*k bytes whose src[] index
+ * frags[]; group_pattern (host, nstripes >> group_shift entries) selects a
+ * pattern per stripe group, or NULL for pattern 0 everywhere. */
+int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes,
+                    uint32_t nfrags, const void *const *frags, void *out,
+                    void *const *outs, uint32_t npatterns, const uint8_t *pats,
+                    const uint8_t *group_pattern, uint32_t group_shift);
+
+/* Pointer classification: index of the (gfx950) device owning device
+ * memory `p`, or -1 for host memory (pageable or pinned). */
+int ecd_ptr_device(const void *p);
+
+/* Pinned host allocation helpers (zero-copy PCIe transfers). */
+void *ecd_host_alloc(size_t bytes);
+void ecd_host_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

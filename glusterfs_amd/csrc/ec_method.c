@@ -1,0 +1,901 @@
+/*
+ * ec_method.c -- host (C) side of the MI355X disperse coder: the drop-in
+ * ec_method_* API of include/ec_method.h.
+ *
+ * What stays on the host, as in the reference, is the O(k^2) scalar work:
+ * GF(2^8) log/exp tables (ec-galois.c:53-70), the encode matrix
+ * (ec-method.c:22-36), the per-mask inverse (ec-method.c:38-72) and the LRU
+ * cache of inverses keyed by brick mask (ec-method.c:134-256).  The per-byte
+ * work -- the reference's row kernels called from ec-method.c:401-407 and
+ * :422-428 -- is handed to the gfx950 kernels through ec_device.h.  There is
+ * no CPU coding path: without a device, ec_method_init() fails.
+ *
+ * Storage contract: only the 120 bytes of the caller's ec_matrix_list_t are
+ * used (ec-types.h:549-562, embedded by value in ec_t at ec-types.h:677):
+ *   lru     -> LRU ring of unreferenced cached inverses (next, prev)
+ *   lock    -> pthread mutex around cache get/put (ec-method.c:206, 250)
+ *   columns/rows/max/count/stripe -> same meaning as the reference
+ *   gf      -> shared GF(2^8) tables          code -> engine context
+ *   encode  -> encode matrix                  objects -> mask-sorted cache
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/ec_method.h"
+#include "ec_device.h"
+
+_Static_assert(sizeof(ec_matrix_list_t) == 120, "ec_matrix_list_t must stay 120 bytes");
+_Static_assert(offsetof(ec_matrix_list_t, columns) == 56, "layout of ec-types.h:549");
+_Static_assert(offsetof(ec_matrix_list_t, objects) == 112, "layout of ec-types.h:561");
+
+#define ECM_MAX_K EC_METHOD_MAX_FRAGMENTS
+#define ECM_MAX_N EC_MI355X_MAX_NODES
+
+/* ------------------------------------------------------------- logging */
+
+static void
+ecm_log(const char *fmt, ...)
+{
+    static int quiet = -1;
+    va_list ap;
+
+    if (quiet < 0) {
+        const char *e = getenv("EC_MI355X_QUIET");
+        quiet = (e && *e && *e != '0') ? 1 : 0;
+    }
+    if (quiet)
+        return;
+    va_start(ap, fmt);
+    fputs("[ec-mi355x] ", stderr);
+    vfprintf(stderr, fmt, ap);
+    fputc('\n', stderr);
+    va_end(ap);
+}
+
+/* ------------------------------------------------------------ GF(2^8) */
+
+typedef struct {
+    uint32_t log[EC_GF_SIZE];
+    uint32_t exp[2 * EC_GF_SIZE]; /* exp[i] = 2^i, doubled to skip a mod */
+} ecm_gf_t;
+
+static ecm_gf_t ecm_gf;
+static pthread_once_t ecm_gf_once = PTHREAD_ONCE_INIT;
+
+/* Generator 2, modulus x^8+x^4+x^3+x^2+1 (EC_GF_MOD, ec-galois.c:59-69). */
+static void
+ecm_gf_build(void)
+{
+    uint32_t i, x = 1;
+
+    for (i = 0; i < EC_GF_SIZE - 1; i++) {
+        ecm_gf.exp[i] = x;
+        ecm_gf.exp[i + EC_GF_SIZE - 1] = x;
+        ecm_gf.log[x] = i;
+        x <<= 1;
+        if (x & EC_GF_SIZE)
+            x ^= EC_GF_MOD;
+    }
+    ecm_gf.log[0] = EC_GF_SIZE; /* undefined; ec-galois.c:61 uses size too */
+}
+
+static const ecm_gf_t *
+ecm_gf_get(void)
+{
+    pthread_once(&ecm_gf_once, ecm_gf_build);
+    return &ecm_gf;
+}
+
+/* ec-galois.c:135-147 semantics (operands >= 256 yield 256). */
+uint32_t
+ec_method_gf_mul(uint32_t a, uint32_t b)
+{
+    const ecm_gf_t *gf = ecm_gf_get();
+
+    if (a >= EC_GF_SIZE || b >= EC_GF_SIZE)
+        return EC_GF_SIZE;
+    if (a == 0 || b == 0)
+        return 0;
+    return gf->exp[gf->log[a] + gf->log[b]];
+}
+
+/* ec-galois.c:149-164 semantics (division by 0 yields 256). */
+uint32_t
+ec_method_gf_div(uint32_t a, uint32_t b)
+{
+    const ecm_gf_t *gf = ecm_gf_get();
+
+    if (a >= EC_GF_SIZE || b >= EC_GF_SIZE || b == 0)
+        return EC_GF_SIZE;
+    if (a == 0)
+        return 0;
+    return gf->exp[gf->log[a] + EC_GF_SIZE - 1 - gf->log[b]];
+}
+
+static uint32_t
+ecm_gf_pow(uint32_t a, uint32_t e)
+{
+    uint32_t r = 1;
+
+    while (e--)
+        r = ec_method_gf_mul(r, a);
+    return r;
+}
+
+/* ----------------------------------------------------------- matrices */
+
+/* Encode row i (brick i) evaluates the data polynomial at v = i + 1 with
+ * the coefficients in reversed order: E[i][j] = v^(k-1-j)
+ * (ec-method.c:22-36 with values[i] = i + 1 from ec-method.c:284-286). */
+int32_t
+ec_method_encode_matrix(uint32_t k, uint32_t n, uint32_t *m)
+{
+    uint32_t i, j;
+
+    if (k < 1 || k > ECM_MAX_K || n < k || n > ECM_MAX_N || !m)
+        return -EINVAL;
+    for (i = 0; i < n; i++)
+        for (j = 0; j < k; j++)
+            m[i * k + j] = ecm_gf_pow(i + 1, k - 1 - j);
+    return 0;
+}
+
+/* Inverse of the k x k reversed-Vandermonde submatrix for the evaluation
+ * points x_p = rows[p] (ec-method.c:38-72 computes the same unique matrix).
+ * Lagrange form: column p holds the coefficients of
+ *   L_p(x) = prod_{q != p} (x + x_q) / prod_{q != p} (x_p + x_q),
+ * highest degree first, so that data_j = sum_p inv[j][p] * fragment_p. */
+int32_t
+ec_method_inverse_matrix(uint32_t k, const uint32_t *rows, uint32_t *inv)
+{
+    uint32_t master[ECM_MAX_K + 1], num[ECM_MAX_K];
+    uint32_t i, j, p, q, den, dinv;
+
+    if (k < 1 || k > ECM_MAX_K || !rows || !inv)
+        return -EINVAL;
+    for (p = 0; p < k; p++) {
+        if (rows[p] == 0 || rows[p] >= EC_GF_SIZE)
+            return -EINVAL;
+        for (q = 0; q < p; q++)
+            if (rows[q] == rows[p])
+                return -EINVAL;
+    }
+    /* master(x) = prod_q (x + x_q); master[d] = coefficient of x^d */
+    memset(master, 0, sizeof(master));
+    master[0] = 1;
+    for (q = 0; q < k; q++) {
+        for (i = q + 1; i > 0; i--)
+            master[i] = master[i - 1] ^ ec_method_gf_mul(master[i], rows[q]);
+        master[0] = ec_method_gf_mul(master[0], rows[q]);
+    }
+    for (p = 0; p < k; p++) {
+        /* num(x) = master(x) / (x + x_p), synthetic division from the top */
+        num[k - 1] = master[k];
+        for (i = k - 1; i > 0; i--)
+            num[i - 1] = master[i] ^ ec_method_gf_mul(num[i], rows[p]);
+        den = 1;
+        for (q = 0; q < k; q++)
+            if (q != p)
+                den = ec_method_gf_mul(den, rows[p] ^ rows[q]);
+        dinv = ec_method_gf_div(1, den);
+        for (j = 0; j < k; j++)
+            inv[j * k + p] = ec_method_gf_mul(num[k - 1 - j], dinv);
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------ engine context */
+
+typedef struct ecm_matrix {
+    struct ecm_matrix *next, *prev; /* LRU links while unreferenced */
+    uint32_t refs;
+    int cached;
+    uintptr_t mask;
+    uint32_t k;
+    uint32_t rows[ECM_MAX_K];
+    uint32_t inv[ECM_MAX_K * ECM_MAX_K];
+} ecm_matrix_t;
+
+typedef struct {
+    uint32_t k, n;
+    uint32_t enc[ECM_MAX_N * ECM_MAX_K];
+    uint8_t enc_pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K]; /* src[k] + n x k */
+    char gen[16];
+} ecm_ctx_t;
+
+#define CTX(list) ((ecm_ctx_t *)(list)->code)
+#define LRU_HEAD(list) ((ecm_matrix_t *)(void *)(list)->lru)
+
+static void
+lru_init(ec_matrix_list_t *list)
+{
+    list->lru[0] = list->lru;
+    list->lru[1] = list->lru;
+}
+
+/* The list head is the two-pointer lru field; matrices link through their
+ * leading next/prev pointers, so the head can be treated as a node. */
+static void
+lru_unlink(ecm_matrix_t *m)
+{
+    m->prev->next = m->next;
+    m->next->prev = m->prev;
+    m->next = m->prev = m;
+}
+
+static void
+lru_push_tail(ec_matrix_list_t *list, ecm_matrix_t *m)
+{
+    ecm_matrix_t *head = LRU_HEAD(list);
+
+    m->next = head;
+    m->prev = head->prev;
+    head->prev->next = m;
+    head->prev = m;
+}
+
+static ecm_matrix_t *
+lru_first(ec_matrix_list_t *list)
+{
+    ecm_matrix_t *head = LRU_HEAD(list);
+
+    return head->next == head ? NULL : head->next;
+}
+
+/* Binary search of the mask-sorted cache (ec-method.c:145-169). */
+static ecm_matrix_t *
+cache_lookup(ec_matrix_list_t *list, uintptr_t mask, uint32_t *pos)
+{
+    ecm_matrix_t **obj = (ecm_matrix_t **)list->objects;
+    uint32_t lo = 0, hi = list->count, mid;
+
+    while (lo < hi) {
+        mid = (lo + hi) >> 1;
+        if (obj[mid]->mask == mask) {
+            *pos = mid;
+            return obj[mid];
+        }
+        if (obj[mid]->mask < mask)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    *pos = lo;
+    return NULL;
+}
+
+static void
+cache_remove(ec_matrix_list_t *list, ecm_matrix_t *m)
+{
+    ecm_matrix_t **obj = (ecm_matrix_t **)list->objects;
+    uint32_t pos;
+
+    if (cache_lookup(list, m->mask, &pos) == m) {
+        list->count--;
+        memmove(obj + pos, obj + pos + 1, sizeof(*obj) * (list->count - pos));
+    }
+    m->cached = 0;
+}
+
+static void
+cache_insert(ec_matrix_list_t *list, ecm_matrix_t *m)
+{
+    ecm_matrix_t **obj = (ecm_matrix_t **)list->objects;
+    uint32_t pos;
+
+    (void)cache_lookup(list, m->mask, &pos);
+    memmove(obj + pos + 1, obj + pos, sizeof(*obj) * (list->count - pos));
+    obj[pos] = m;
+    list->count++;
+    m->cached = 1;
+}
+
+static int
+mask_rows_ok(const ec_matrix_list_t *list, uintptr_t mask, const uint32_t *rows)
+{
+    uint32_t p, bits = 0;
+    uintptr_t seen = 0;
+
+    for (p = 0; p < list->rows && p < sizeof(uintptr_t) * 8; p++)
+        bits += (mask >> p) & 1;
+    if (bits != list->columns || (mask >> list->rows) != 0)
+        return 0;
+    for (p = 0; p < list->columns; p++) {
+        if (rows[p] < 1 || rows[p] > list->rows)
+            return 0;
+        if (p && rows[p] <= rows[p - 1])
+            return 0;
+        seen |= (uintptr_t)1 << (rows[p] - 1);
+    }
+    return seen == mask;
+}
+
+static void
+rows_from_mask(uintptr_t mask, uint32_t *rows)
+{
+    uint32_t i, p = 0;
+
+    for (i = 0; i < sizeof(uintptr_t) * 8; i++)
+        if ((mask >> i) & 1)
+            rows[p++] = i + 1;
+}
+
+/* ec-method.c:200-245: cached inverse for `mask`, refcount held. */
+static ecm_matrix_t *
+matrix_get(ec_matrix_list_t *list, uintptr_t mask, const uint32_t *rows)
+{
+    ecm_matrix_t *m;
+    uint32_t pos;
+
+    pthread_mutex_lock(&list->lock);
+    m = cache_lookup(list, mask, &pos);
+    if (m) {
+        if (m->refs++ == 0)
+            lru_unlink(m);
+        pthread_mutex_unlock(&list->lock);
+        return m;
+    }
+    if (list->count >= list->max && (m = lru_first(list)) != NULL) {
+        lru_unlink(m);
+        cache_remove(list, m);
+    } else {
+        m = (ecm_matrix_t *)calloc(1, sizeof(*m));
+        if (!m) {
+            pthread_mutex_unlock(&list->lock);
+            return NULL;
+        }
+    }
+    m->next = m->prev = m;
+    m->refs = 1;
+    m->mask = mask;
+    m->k = list->columns;
+    memcpy(m->rows, rows, sizeof(uint32_t) * list->columns);
+    ec_method_inverse_matrix(list->columns, rows, m->inv);
+    if (list->count < list->max)
+        cache_insert(list, m);
+    pthread_mutex_unlock(&list->lock);
+    return m;
+}
+
+/* ec-method.c:247-255 / :133-143 */
+static void
+matrix_put(ec_matrix_list_t *list, ecm_matrix_t *m)
+{
+    pthread_mutex_lock(&list->lock);
+    if (--m->refs == 0) {
+        if (m->cached)
+            lru_push_tail(list, m);
+        else
+            free(m);
+    }
+    pthread_mutex_unlock(&list->lock);
+}
+
+/* Pack {src[k], coef[rows][k]} for the combine kernel. */
+static uint32_t
+pack_pattern(uint8_t *dst, uint32_t k, const uint8_t *src, uint32_t rows,
+             const uint32_t *coef)
+{
+    uint32_t i;
+
+    memcpy(dst, src, k);
+    for (i = 0; i < rows * k; i++)
+        dst[k + i] = (uint8_t)coef[i];
+    return k + rows * k;
+}
+
+/* ------------------------------------------------------------ the API */
+
+int32_t
+ec_method_device_count(void)
+{
+    return ecd_device_count();
+}
+
+const char *
+ec_method_last_error(void)
+{
+    return ecd_last_error();
+}
+
+void *
+ec_method_host_alloc(size_t bytes)
+{
+    return ecd_host_alloc(bytes);
+}
+
+void
+ec_method_host_free(void *p)
+{
+    ecd_host_free(p);
+}
+
+static const char *const ecm_known_gens[] = {"none", "auto", "x64", "sse", "avx", "hip",
+                                             NULL};
+
+int32_t
+ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t rows,
+               uint32_t max, const char *gen)
+{
+    ecm_ctx_t *ctx;
+    uint32_t i;
+    int known = 0;
+
+    (void)xl;
+    if (!list)
+        return -EINVAL;
+    memset(list, 0, sizeof(*list));
+    if (columns < 1 || columns > ECM_MAX_K || rows < columns || rows > ECM_MAX_N)
+        return -EINVAL;
+    if (ecd_device_count() == 0) {
+        ecm_log("no MI355X (gfx950) device: %s; refusing to start (no CPU path)",
+                ecd_last_error());
+        return -ENODEV;
+    }
+    for (i = 0; gen && ecm_known_gens[i]; i++)
+        known |= strcmp(gen, ecm_known_gens[i]) == 0;
+    if (gen && !known)
+        ecm_log("unknown cpu-extensions value '%s', using the gfx950 engine", gen);
+
+    ctx = (ecm_ctx_t *)calloc(1, sizeof(*ctx));
+    list->objects = (void **)calloc(max ? max : 1, sizeof(void *));
+    if (!ctx || !list->objects) {
+        free(ctx);
+        free(list->objects);
+        list->objects = NULL;
+        return -ENOMEM;
+    }
+    ctx->k = columns;
+    ctx->n = rows;
+    snprintf(ctx->gen, sizeof(ctx->gen), "%s", gen ? gen : "auto");
+    ec_method_encode_matrix(columns, rows, ctx->enc);
+    {
+        uint8_t src[ECM_MAX_K];
+        for (i = 0; i < columns; i++)
+            src[i] = (uint8_t)i;
+        pack_pattern(ctx->enc_pat, columns, src, rows, ctx->enc);
+    }
+
+    list->columns = columns;
+    list->rows = rows;
+    list->max = max;
+    list->count = 0;
+    list->stripe = EC_METHOD_CHUNK_SIZE * columns;
+    list->gf = (void *)ecm_gf_get();
+    list->code = ctx;
+    list->encode = ctx->enc;
+    lru_init(list);
+    pthread_mutex_init(&list->lock, NULL);
+    ecm_log("disperse %u+%u on %d MI355X device(s) (cpu-extensions=%s -> gfx950 %s)",
+            columns, rows - columns, ecd_device_count(), ctx->gen,
+            ecd_has_vander(columns, rows) ? "specialised encoder" : "generic encoder");
+    return 0;
+}
+
+void
+ec_method_fini(ec_matrix_list_t *list)
+{
+    ecm_matrix_t *m;
+
+    if (!list || !list->code)
+        return;
+    while ((m = lru_first(list)) != NULL) {
+        lru_unlink(m);
+        cache_remove(list, m);
+        free(m);
+    }
+    /* referenced matrices cannot exist here: callers hold refs only inside
+     * a decode call (ec-method.c:369 asserts the same) */
+    pthread_mutex_destroy(&list->lock);
+    free(list->objects);
+    free(list->code);
+    memset(list, 0, sizeof(*list));
+}
+
+int32_t
+ec_method_update(xlator_t *xl, ec_matrix_list_t *list, const char *gen)
+{
+    (void)xl;
+    (void)list;
+    (void)gen;
+    return 0;
+}
+
+static int
+encode_any(ec_matrix_list_t *list, uint64_t nstripes, const void *in, void *const *out)
+{
+    ecm_ctx_t *ctx = CTX(list);
+    int dev;
+    uint32_t i;
+
+    if (nstripes == 0)
+        return 0;
+    dev = ecd_ptr_device(in);
+    if (dev >= 0) {
+        for (i = 0; i < ctx->n; i++)
+            if (ecd_ptr_device(out[i]) != dev)
+                return -EINVAL;
+        int rc = ec_method_encode_device(list, dev, NULL, nstripes, in, out);
+        return rc ? rc : ecd_sync(dev, NULL);
+    }
+    for (i = 0; i < ctx->n; i++)
+        if (ecd_ptr_device(out[i]) >= 0)
+            return -EINVAL; /* mixed host/device buffers are not supported */
+    return ecd_encode_host(0, ctx->k, ctx->n, nstripes, in, out, ctx->enc_pat);
+}
+
+void
+ec_method_encode(ec_matrix_list_t *list, uint64_t size, void *in, void **out)
+{
+    ecm_ctx_t *ctx = CTX(list);
+    uint32_t i;
+    int rc;
+
+    if (!ctx || size % list->stripe != 0) {
+        ecm_log("ec_method_encode: size %llu is not a multiple of the stripe (%u)",
+                (unsigned long long)size, list->stripe);
+        abort();
+    }
+    rc = encode_any(list, size / list->stripe, in, out);
+    if (rc != 0) {
+        ecm_log("ec_method_encode failed (%d): %s", rc, ecd_last_error());
+        abort(); /* the reference's encode cannot fail; never return bad data */
+    }
+    for (i = 0; i < ctx->n; i++)
+        out[i] = (uint8_t *)out[i] + size / list->columns;
+}
+
+int32_t
+ec_method_encode_batch(ec_matrix_list_t *list, uint64_t nstripes, const void *in,
+                       void *const *out)
+{
+    if (!list || !CTX(list) || (!in && nstripes) || (!out && nstripes))
+        return -EINVAL;
+    return encode_any(list, nstripes, in, out);
+}
+
+static int
+decode_any(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask, const uint32_t *rows,
+           const void *const *in, void *out)
+{
+    uint8_t pat[ECM_MAX_K + ECM_MAX_K * ECM_MAX_K];
+    uint8_t src[ECM_MAX_K];
+    ecm_matrix_t *m;
+    uint32_t k = list->columns, p;
+    int dev, rc;
+
+    if (!mask_rows_ok(list, mask, rows))
+        return -EINVAL;
+    if (nstripes == 0)
+        return 0;
+    dev = ecd_ptr_device(out);
+    if (dev >= 0) {
+        for (p = 0; p < k; p++)
+            if (ecd_ptr_device(in[p]) != dev)
+                return -EINVAL;
+        rc = ec_method_decode_device(list, dev, NULL, nstripes, mask, in, out);
+        return rc ? rc : ecd_sync(dev, NULL);
+    }
+    for (p = 0; p < k; p++)
+        if (ecd_ptr_device(in[p]) >= 0)
+            return -EINVAL;
+    m = matrix_get(list, mask, rows);
+    if (!m)
+        return -ENOMEM;
+    for (p = 0; p < k; p++)
+        src[p] = (uint8_t)p;
+    pack_pattern(pat, k, src, k, m->inv);
+    matrix_put(list, m);
+    return ecd_decode_host(0, k, k, nstripes, k, in, out, NULL, 1, pat, NULL, 0);
+}
+
+int32_t
+ec_method_decode(ec_matrix_list_t *list, uint64_t size, uintptr_t mask, uint32_t *rows,
+                 void **in, void *out)
+{
+    if (!list || !CTX(list) || size % EC_METHOD_CHUNK_SIZE != 0 || !rows || !in ||
+        (!out && size))
+        return -EINVAL;
+    return decode_any(list, size / EC_METHOD_CHUNK_SIZE, mask, rows,
+                      (const void *const *)in, out);
+}
+
+int32_t
+ec_method_decode_batch(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
+                       const uint32_t *rows, const void *const *in, void *out)
+{
+    if (!list || !CTX(list) || !rows || !in || (!out && nstripes))
+        return -EINVAL;
+    return decode_any(list, nstripes, mask, rows, in, out);
+}
+
+/* Build the packed pattern for `mask` reading from the n-fragment array. */
+static int
+mask_pattern(ec_matrix_list_t *list, uintptr_t mask, uint8_t *pat)
+{
+    uint32_t rows[ECM_MAX_K];
+    uint8_t src[ECM_MAX_K];
+    ecm_matrix_t *m;
+    uint32_t p, k = list->columns;
+
+    rows_from_mask(mask, rows);
+    if (!mask_rows_ok(list, mask, rows))
+        return -EINVAL;
+    m = matrix_get(list, mask, rows);
+    if (!m)
+        return -ENOMEM;
+    for (p = 0; p < k; p++)
+        src[p] = (uint8_t)(rows[p] - 1);
+    pack_pattern(pat, k, src, k, m->inv);
+    matrix_put(list, m);
+    return 0;
+}
+
+int32_t
+ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_stripes,
+                       const uintptr_t *group_masks, const void *const *frags, void *out)
+{
+    uint8_t pats[ECD_MAX_PAT_BYTES];
+    uintptr_t uniq[256];
+    uint8_t *gp;
+    uint64_t g, ngroups;
+    uint32_t shift = 0, nu = 0, u, k, pb;
+    int rc;
+
+    if (!list || !CTX(list) || !group_masks || !frags || (!out && nstripes))
+        return -EINVAL;
+    if (group_stripes < 8 || (group_stripes & (group_stripes - 1)))
+        return -EINVAL;
+    while ((1ull << shift) < group_stripes)
+        shift++;
+    if (nstripes == 0)
+        return 0;
+    k = list->columns;
+    pb = k + k * k;
+    ngroups = (nstripes + group_stripes - 1) / group_stripes;
+    gp = (uint8_t *)malloc(ngroups);
+    if (!gp)
+        return -ENOMEM;
+    rc = 0;
+    for (g = 0; g < ngroups && rc == 0; g++) {
+        for (u = 0; u < nu; u++)
+            if (uniq[u] == group_masks[g])
+                break;
+        if (u == nu) {
+            if ((nu + 1) * pb > ECD_MAX_PAT_BYTES || nu == 256) {
+                rc = -E2BIG;
+                break;
+            }
+            rc = mask_pattern(list, group_masks[g], pats + nu * pb);
+            uniq[nu++] = group_masks[g];
+        }
+        gp[g] = (uint8_t)u;
+    }
+    if (rc == 0)
+        rc = ecd_decode_host(0, k, k, nstripes, list->rows, frags, out, NULL, nu, pats, gp,
+                             shift);
+    free(gp);
+    return rc;
+}
+
+/* Heal matrix: rows of the encode matrix for the target bricks times the
+ * inverse for `mask` -> m x k coefficients applied to the k fragments. */
+static int
+heal_pattern(ec_matrix_list_t *list, uintptr_t mask, const uint32_t *rows,
+             uintptr_t target_mask, uint8_t *pat, uint32_t *ntargets)
+{
+    ecm_ctx_t *ctx = CTX(list);
+    uint32_t coef[ECM_MAX_N * ECM_MAX_K];
+    uint8_t src[ECM_MAX_K];
+    ecm_matrix_t *m;
+    uint32_t k = list->columns, t = 0, i, j, p, acc;
+
+    if ((target_mask >> list->rows) != 0 || target_mask == 0)
+        return -EINVAL;
+    m = matrix_get(list, mask, rows);
+    if (!m)
+        return -ENOMEM;
+    for (i = 0; i < list->rows; i++) {
+        if (!((target_mask >> i) & 1))
+            continue;
+        for (p = 0; p < k; p++) {
+            acc = 0;
+            for (j = 0; j < k; j++)
+                acc ^= ec_method_gf_mul(ctx->enc[i * k + j], m->inv[j * k + p]);
+            coef[t * k + p] = acc;
+        }
+        t++;
+    }
+    matrix_put(list, m);
+    for (p = 0; p < k; p++)
+        src[p] = (uint8_t)p;
+    pack_pattern(pat, k, src, t, coef);
+    *ntargets = t;
+    return 0;
+}
+
+int32_t
+ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
+               const void *const *in, uintptr_t target_mask, void *const *out)
+{
+    uint8_t pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K];
+    uint32_t rows[ECM_MAX_K], nt = 0, p;
+    int dev, rc;
+
+    if (!list || !CTX(list) || !in || !out)
+        return -EINVAL;
+    rows_from_mask(mask, rows);
+    if (!mask_rows_ok(list, mask, rows))
+        return -EINVAL;
+    if (nstripes == 0)
+        return 0;
+    dev = ecd_ptr_device(in[0]);
+    if (dev >= 0) {
+        rc = ec_method_heal_device(list, dev, NULL, nstripes, mask, in, target_mask, out);
+        return rc ? rc : ecd_sync(dev, NULL);
+    }
+    for (p = 0; p < list->columns; p++)
+        if (ecd_ptr_device(in[p]) >= 0)
+            return -EINVAL;
+    rc = heal_pattern(list, mask, rows, target_mask, pat, &nt);
+    if (rc)
+        return rc;
+    return ecd_decode_host(0, list->columns, nt, nstripes, list->columns, in, NULL, out, 1,
+                           pat, NULL, 0);
+}
+
+/* ---------------------------------------------------- device-resident */
+
+static void
+desc_init(ecd_combine_desc_t *d, uint32_t k, uint32_t rows, uint64_t nstripes)
+{
+    memset(d, 0, offsetof(ecd_combine_desc_t, pat));
+    d->k = k;
+    d->rows = rows;
+    d->nstripes = nstripes;
+    d->npatterns = 1;
+    d->pat_bytes = k + rows * k;
+}
+
+int32_t
+ec_method_encode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                        const void *in, void *const *out)
+{
+    ecm_ctx_t *ctx;
+    ecd_combine_desc_t d;
+    uint32_t p;
+
+    if (!list || !(ctx = CTX(list)) || !in || !out)
+        return -EINVAL;
+    if (nstripes == 0)
+        return 0;
+    if (ecd_has_vander(ctx->k, ctx->n))
+        return ecd_encode_vander(device, stream, ctx->k, ctx->n, nstripes, in, out);
+    desc_init(&d, ctx->k, ctx->n, nstripes);
+    d.in_stride = (uint64_t)ctx->k * EC_METHOD_CHUNK_SIZE;
+    d.out_stride = EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < ctx->k; p++)
+        d.in_base[p] = (const uint8_t *)in + (uint64_t)p * EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < ctx->n; p++)
+        d.out_base[p] = out[p];
+    memcpy(d.pat, ctx->enc_pat, d.pat_bytes);
+    return ecd_combine(device, stream, &d);
+}
+
+int32_t
+ec_method_decode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                        uintptr_t mask, const void *const *in, void *out)
+{
+    uint32_t rows[ECM_MAX_K], k, p, r;
+    uint8_t src[ECM_MAX_K];
+    ecd_combine_desc_t d;
+    ecm_matrix_t *m;
+
+    if (!list || !CTX(list) || !in || !out)
+        return -EINVAL;
+    k = list->columns;
+    rows_from_mask(mask, rows);
+    if (!mask_rows_ok(list, mask, rows))
+        return -EINVAL;
+    if (nstripes == 0)
+        return 0;
+    m = matrix_get(list, mask, rows);
+    if (!m)
+        return -ENOMEM;
+    desc_init(&d, k, k, nstripes);
+    d.in_stride = EC_METHOD_CHUNK_SIZE;
+    d.out_stride = (uint64_t)k * EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < k; p++) {
+        d.in_base[p] = in[p];
+        src[p] = (uint8_t)p;
+    }
+    for (r = 0; r < k; r++)
+        d.out_base[r] = (uint8_t *)out + (uint64_t)r * EC_METHOD_CHUNK_SIZE;
+    pack_pattern(d.pat, k, src, k, m->inv);
+    matrix_put(list, m);
+    return ecd_combine(device, stream, &d);
+}
+
+int32_t
+ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
+                              uint64_t nstripes, uint64_t group_stripes,
+                              const uint8_t *group_pattern, uint32_t nmasks,
+                              const uintptr_t *masks, const void *const *frags, void *out)
+{
+    ecd_combine_desc_t d;
+    uint32_t k, r, u, shift = 0;
+    int rc;
+
+    if (!list || !CTX(list) || !group_pattern || !masks || !frags || !out || nmasks == 0)
+        return -EINVAL;
+    if (group_stripes < 8 || (group_stripes & (group_stripes - 1)))
+        return -EINVAL;
+    while ((1ull << shift) < group_stripes)
+        shift++;
+    k = list->columns;
+    if ((uint64_t)nmasks * (k + k * k) > ECD_MAX_PAT_BYTES)
+        return -E2BIG;
+    if (nstripes == 0)
+        return 0;
+    desc_init(&d, k, k, nstripes);
+    d.npatterns = nmasks;
+    d.in_stride = EC_METHOD_CHUNK_SIZE;
+    d.out_stride = (uint64_t)k * EC_METHOD_CHUNK_SIZE;
+    for (u = 0; u < list->rows; u++)
+        d.in_base[u] = frags[u];
+    for (r = 0; r < k; r++)
+        d.out_base[r] = (uint8_t *)out + (uint64_t)r * EC_METHOD_CHUNK_SIZE;
+    for (u = 0; u < nmasks; u++) {
+        rc = mask_pattern(list, masks[u], d.pat + u * d.pat_bytes);
+        if (rc)
+            return rc;
+    }
+    d.group_pattern = group_pattern;
+    d.group_shift = shift;
+    return ecd_combine(device, stream, &d);
+}
+
+int32_t
+ec_method_heal_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                      uintptr_t mask, const void *const *in, uintptr_t target_mask,
+                      void *const *out)
+{
+    uint32_t rows[ECM_MAX_K], nt = 0, p;
+    ecd_combine_desc_t d;
+    int rc;
+
+    if (!list || !CTX(list) || !in || !out)
+        return -EINVAL;
+    rows_from_mask(mask, rows);
+    if (!mask_rows_ok(list, mask, rows))
+        return -EINVAL;
+    if (nstripes == 0)
+        return 0;
+    memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
+    rc = heal_pattern(list, mask, rows, target_mask, d.pat, &nt);
+    if (rc)
+        return rc;
+    d.k = list->columns;
+    d.rows = nt;
+    d.nstripes = nstripes;
+    d.npatterns = 1;
+    d.pat_bytes = d.k + nt * d.k;
+    d.in_stride = EC_METHOD_CHUNK_SIZE;
+    d.out_stride = EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < d.k; p++)
+        d.in_base[p] = in[p];
+    for (p = 0; p < nt; p++)
+        d.out_base[p] = out[p];
+    return ecd_combine(device, stream, &d);
+}
+
+int32_t
+ec_method_sync_device(int device, void *stream)
+{
+    return ecd_sync(device, stream);
+}

@@ -1,0 +1,270 @@
+"""Python mirror of the disperse coder's C ABI (include/ec_method.h).
+
+This is a thin ctypes layer over glusterfs_amd/lib/libec_mi355x.so with the
+same names, argument meaning and error behaviour as the reference's
+ec-method.h:31-46 (ec_method_init / fini / update / encode / decode), plus the
+batched, mixed-pattern, heal and device-resident entry points.  Negative
+errno returns become ``OSError(errno)``; ``ec_method_encode`` mirrors the
+reference's ``void`` signature.
+
+Buffers can be numpy arrays, torch tensors (host or device), ctypes buffers or
+plain integer addresses.  There is no Python or CPU coding fallback: if the
+library is missing, importing this module raises.
+"""
+import ctypes
+import errno
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libec_mi355x.so")
+
+EC_GF_BITS = 8
+EC_GF_MOD = 0x11D
+EC_METHOD_MAX_FRAGMENTS = 16
+EC_METHOD_WORD_SIZE = 64
+EC_METHOD_CHUNK_SIZE = EC_METHOD_WORD_SIZE * EC_GF_BITS
+EC_MAX_NODES = 31
+
+# Every symbol include/ec_method.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "ec_method_init", "ec_method_fini", "ec_method_update", "ec_method_encode",
+    "ec_method_decode", "ec_method_encode_batch", "ec_method_decode_batch",
+    "ec_method_decode_mixed", "ec_method_heal", "ec_method_encode_device",
+    "ec_method_decode_device", "ec_method_decode_mixed_device",
+    "ec_method_heal_device", "ec_method_sync_device", "ec_method_device_count",
+    "ec_method_last_error", "ec_method_host_alloc", "ec_method_host_free",
+    "ec_method_encode_matrix", "ec_method_inverse_matrix", "ec_method_gf_mul",
+    "ec_method_gf_div",
+)
+
+
+class MatrixList(ctypes.Structure):
+    """ec_matrix_list_t storage (120 bytes, layout of ec-types.h:549-562)."""
+    _fields_ = [
+        ("lru", ctypes.c_void_p * 2),
+        ("lock", ctypes.c_byte * 40),
+        ("columns", ctypes.c_uint32),
+        ("rows", ctypes.c_uint32),
+        ("max", ctypes.c_uint32),
+        ("count", ctypes.c_uint32),
+        ("stripe", ctypes.c_uint32),
+        ("pool", ctypes.c_void_p),
+        ("gf", ctypes.c_void_p),
+        ("code", ctypes.c_void_p),
+        ("encode", ctypes.c_void_p),
+        ("objects", ctypes.c_void_p),
+    ]
+
+
+assert ctypes.sizeof(MatrixList) == 120
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libec_mi355x.so not built (%s); run `make -C glusterfs_amd` or "
+            "__graft_entry__.build() -- there is no CPU fallback" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    up = ctypes.c_size_t  # uintptr_t
+    P = ctypes.POINTER(MatrixList)
+    sig = {
+        "ec_method_init": (i32, [vp, P, u32, u32, u32, ctypes.c_char_p]),
+        "ec_method_fini": (None, [P]),
+        "ec_method_update": (i32, [vp, P, ctypes.c_char_p]),
+        "ec_method_encode": (None, [P, u64, vp, vp]),
+        "ec_method_decode": (i32, [P, u64, up, vp, vp, vp]),
+        "ec_method_encode_batch": (i32, [P, u64, vp, vp]),
+        "ec_method_decode_batch": (i32, [P, u64, up, vp, vp, vp]),
+        "ec_method_decode_mixed": (i32, [P, u64, u64, vp, vp, vp]),
+        "ec_method_heal": (i32, [P, u64, up, vp, up, vp]),
+        "ec_method_encode_device": (i32, [P, ctypes.c_int, vp, u64, vp, vp]),
+        "ec_method_decode_device": (i32, [P, ctypes.c_int, vp, u64, up, vp, vp]),
+        "ec_method_decode_mixed_device": (i32, [P, ctypes.c_int, vp, u64, u64, vp, u32, vp,
+                                                vp, vp]),
+        "ec_method_heal_device": (i32, [P, ctypes.c_int, vp, u64, up, vp, up, vp]),
+        "ec_method_sync_device": (i32, [ctypes.c_int, vp]),
+        "ec_method_device_count": (i32, []),
+        "ec_method_last_error": (ctypes.c_char_p, []),
+        "ec_method_host_alloc": (vp, [ctypes.c_size_t]),
+        "ec_method_host_free": (None, [vp]),
+        "ec_method_encode_matrix": (i32, [u32, u32, vp]),
+        "ec_method_inverse_matrix": (i32, [u32, vp, vp]),
+        "ec_method_gf_mul": (u32, [u32, u32]),
+        "ec_method_gf_div": (u32, [u32, u32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+lib = _load()
+
+
+def addr(buf):
+    """Address of a buffer: numpy array, torch tensor, ctypes object or int."""
+    if buf is None:
+        return None
+    if isinstance(buf, int):
+        return buf
+    if hasattr(buf, "data_ptr"):          # torch.Tensor
+        return buf.data_ptr()
+    if hasattr(buf, "ctypes"):            # numpy.ndarray
+        return buf.ctypes.data
+    return ctypes.addressof(buf)
+
+
+def _ptr_array(bufs):
+    return (ctypes.c_void_p * len(bufs))(*[addr(b) for b in bufs])
+
+
+def _check(rc, what):
+    if rc != 0:
+        err = -rc if rc < 0 else errno.EIO
+        raise OSError(err, "%s failed: %s (%s)" % (what, os.strerror(err),
+                                                   (lib.ec_method_last_error() or b"").decode()))
+    return rc
+
+
+def device_count():
+    return lib.ec_method_device_count()
+
+
+def gf_mul(a, b):
+    return lib.ec_method_gf_mul(a, b)
+
+
+def gf_div(a, b):
+    return lib.ec_method_gf_div(a, b)
+
+
+def encode_matrix(columns, rows):
+    m = (ctypes.c_uint32 * (columns * rows))()
+    _check(lib.ec_method_encode_matrix(columns, rows, m), "ec_method_encode_matrix")
+    return [[m[i * columns + j] for j in range(columns)] for i in range(rows)]
+
+
+def inverse_matrix(rows):
+    k = len(rows)
+    r = (ctypes.c_uint32 * k)(*rows)
+    m = (ctypes.c_uint32 * (k * k))()
+    _check(lib.ec_method_inverse_matrix(k, r, m), "ec_method_inverse_matrix")
+    return [[m[i * k + j] for j in range(k)] for i in range(k)]
+
+
+def mask_rows(mask):
+    """Brick mask -> ascending rows (brick index + 1), as ec-inode-read.c:1174."""
+    return [i + 1 for i in range(64) if (mask >> i) & 1]
+
+
+class ECMatrixList:
+    """An initialised ec_matrix_list_t: the coder of one disperse volume.
+
+    Mirrors ec-method.h: ``ECMatrixList(columns=k, rows=n, max=2n, gen)`` is
+    ec_method_init (ec.c:837), ``fini()`` ec_method_fini, ``encode`` and
+    ``decode`` the two hot-path calls (ec-inode-write.c:2136,
+    ec-inode-read.c:1196)."""
+
+    def __init__(self, columns, rows, max=None, gen="auto"):
+        self.columns, self.rows = columns, rows
+        self.max = 2 * rows if max is None else max
+        self._list = MatrixList()
+        self._live = False
+        rc = lib.ec_method_init(None, ctypes.byref(self._list), columns, rows, self.max,
+                                gen.encode() if gen is not None else None)
+        _check(rc, "ec_method_init")
+        self._live = True
+
+    # --- reference surface -------------------------------------------------
+    @property
+    def stripe(self):
+        return self._list.stripe
+
+    @property
+    def count(self):
+        return self._list.count
+
+    def fini(self):
+        if self._live:
+            lib.ec_method_fini(ctypes.byref(self._list))
+            self._live = False
+
+    def __del__(self):
+        try:
+            self.fini()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.fini()
+
+    def update(self, gen):
+        return _check(lib.ec_method_update(None, ctypes.byref(self._list), gen.encode()),
+                      "ec_method_update")
+
+    def encode(self, size, inp, out):
+        """ec_method_encode: `out` is a list of n fragment buffers."""
+        ptrs = _ptr_array(out)
+        lib.ec_method_encode(ctypes.byref(self._list), size, addr(inp), ptrs)
+
+    def decode(self, size, mask, rows, inp, out):
+        """ec_method_decode: size = bytes per fragment; rows = brick idx + 1."""
+        r = (ctypes.c_uint32 * len(rows))(*rows)
+        return _check(lib.ec_method_decode(ctypes.byref(self._list), size, mask, r,
+                                           _ptr_array(inp), addr(out)), "ec_method_decode")
+
+    # --- batched / new -------------------------------------------------------
+    def encode_batch(self, nstripes, inp, out):
+        return _check(lib.ec_method_encode_batch(ctypes.byref(self._list), nstripes,
+                                                 addr(inp), _ptr_array(out)),
+                      "ec_method_encode_batch")
+
+    def decode_batch(self, nstripes, mask, rows, inp, out):
+        r = (ctypes.c_uint32 * len(rows))(*rows)
+        return _check(lib.ec_method_decode_batch(ctypes.byref(self._list), nstripes, mask, r,
+                                                 _ptr_array(inp), addr(out)),
+                      "ec_method_decode_batch")
+
+    def decode_mixed(self, nstripes, group_stripes, group_masks, frags, out):
+        gm = (ctypes.c_size_t * len(group_masks))(*group_masks)
+        return _check(lib.ec_method_decode_mixed(ctypes.byref(self._list), nstripes,
+                                                 group_stripes, gm, _ptr_array(frags),
+                                                 addr(out)), "ec_method_decode_mixed")
+
+    def heal(self, nstripes, mask, inp, target_mask, out):
+        return _check(lib.ec_method_heal(ctypes.byref(self._list), nstripes, mask,
+                                         _ptr_array(inp), target_mask, _ptr_array(out)),
+                      "ec_method_heal")
+
+    # --- device-resident, asynchronous --------------------------------------
+    def encode_device(self, device, stream, nstripes, inp, out):
+        return _check(lib.ec_method_encode_device(ctypes.byref(self._list), device, stream,
+                                                  nstripes, addr(inp), _ptr_array(out)),
+                      "ec_method_encode_device")
+
+    def decode_device(self, device, stream, nstripes, mask, inp, out):
+        return _check(lib.ec_method_decode_device(ctypes.byref(self._list), device, stream,
+                                                  nstripes, mask, _ptr_array(inp),
+                                                  addr(out)), "ec_method_decode_device")
+
+    def decode_mixed_device(self, device, stream, nstripes, group_stripes, group_pattern,
+                            masks, frags, out):
+        m = (ctypes.c_size_t * len(masks))(*masks)
+        return _check(lib.ec_method_decode_mixed_device(
+            ctypes.byref(self._list), device, stream, nstripes, group_stripes,
+            addr(group_pattern), len(masks), m, _ptr_array(frags), addr(out)),
+            "ec_method_decode_mixed_device")
+
+    def heal_device(self, device, stream, nstripes, mask, inp, target_mask, out):
+        return _check(lib.ec_method_heal_device(ctypes.byref(self._list), device, stream,
+                                                nstripes, mask, _ptr_array(inp), target_mask,
+                                                _ptr_array(out)), "ec_method_heal_device")
+
+
+def sync_device(device, stream=None):
+    return _check(lib.ec_method_sync_device(device, stream), "ec_method_sync_device")

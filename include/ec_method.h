@@ -1,0 +1,181 @@
+/*
+ * ec_method.h -- drop-in C ABI of the MI355X (gfx950) disperse coder.
+ *
+ * This library (glusterfs_amd/lib/libec_mi355x.so) replaces the coding layer
+ * of GlusterFS's disperse translator: ec-method.c, ec-code*.c, ec-galois.c and
+ * ec-gf8.c in xlators/cluster/ec/src.  The five ec_method_* prototypes below
+ * are exactly those of ec-method.h:31-46, with the same argument meaning,
+ * return conventions (0 / negative errno) and data layout (512-byte chunks of
+ * 8 bit-planes x 64 bytes, EC_METHOD_CHUNK_SIZE), so ec.c, ec-inode-write.c,
+ * ec-inode-read.c and ec-heal.c link against it unchanged.
+ *
+ * Data buffers may be host memory (pageable or pinned) or MI355X device
+ * memory; host data crosses PCIe inside the call.  There is no CPU coding
+ * path: without a gfx950 device ec_method_init() fails with -ENODEV.
+ */
+#ifndef EC_MI355X_EC_METHOD_H
+#define EC_MI355X_EC_METHOD_H
+
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Constants of ec-method.h:17-29. */
+#define EC_GF_BITS 8
+#define EC_GF_MOD 0x11D
+#define EC_GF_SIZE (1 << EC_GF_BITS)
+#define EC_METHOD_MAX_FRAGMENTS 16
+#define EC_METHOD_MAX_NODES (EC_GF_SIZE - 1)
+#define EC_METHOD_WORD_SIZE 64
+#define EC_METHOD_CHUNK_SIZE (EC_METHOD_WORD_SIZE * EC_GF_BITS)
+
+/* Largest brick count the library accepts (EC_MAX_NODES, ec.h:27-32). */
+#define EC_MI355X_MAX_NODES 31
+
+#ifndef __EC_TYPES_H__
+/* Standalone declarations.  Inside GlusterFS, ec-types.h (included first)
+ * provides the real definitions; the layout below is byte-compatible with
+ * ec-types.h:549-562 (sizeof == 120 on LP64, same field offsets), which is
+ * the only storage the library uses: the caller embeds the list by value in
+ * ec_t (ec-types.h:677). */
+typedef struct _xlator xlator_t;
+typedef struct _ec_matrix_list ec_matrix_list_t;
+
+struct _ec_matrix_list {
+    void *lru[2];           /* struct list_head lru           @0   */
+    pthread_mutex_t lock;   /* gf_lock_t lock                 @16  */
+    uint32_t columns;       /* k                              @56  */
+    uint32_t rows;          /* n                              @60  */
+    uint32_t max;           /* decode-matrix cache capacity   @64  */
+    uint32_t count;         /* cached decode matrices         @68  */
+    uint32_t stripe;        /* EC_METHOD_CHUNK_SIZE * k       @72  */
+    void *pool;             /* struct mem_pool *pool          @80  */
+    void *gf;               /* ec_gf_t *gf                    @88  */
+    void *code;             /* ec_code_t *code                @96  */
+    void *encode;           /* ec_matrix_t *encode            @104 */
+    void **objects;         /* ec_matrix_t **objects          @112 */
+};
+#endif
+
+/* ------------------------------------------------------------------------
+ * Drop-in entry points (ec-method.h:31-46).
+ * --------------------------------------------------------------------- */
+
+/* Replaces ec-method.c:299-353, called from ec.c:837.  columns = k data
+ * fragments, rows = n bricks, max = decode matrix cache size (2n in ec.c),
+ * gen = the disperse.cpu-extensions value (ec.c:1786-1794: none, auto, x64,
+ * sse, avx) or "hip"; every value selects the gfx950 engine.  Returns 0,
+ * -EINVAL (bad geometry), -ENOMEM, or -ENODEV (no MI355X visible). */
+int32_t ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns,
+                       uint32_t rows, uint32_t max, const char *gen);
+
+/* Replaces ec-method.c:355-383 (ec.c:198).  Safe on a list whose init failed. */
+void ec_method_fini(ec_matrix_list_t *list);
+
+/* Replaces ec-method.c:385-391 (ec.c:293): a no-op returning 0, as in the
+ * reference (changing the engine needs a remount there too). */
+int32_t ec_method_update(xlator_t *xl, ec_matrix_list_t *list, const char *gen);
+
+/* Replaces ec-method.c:393-408 (ec-inode-write.c:2136).  size: user bytes,
+ * a multiple of EC_METHOD_CHUNK_SIZE * k.  out[i] receives size/k bytes of
+ * fragment i and, as in the reference, each out[i] is advanced by size/k.
+ * The reference cannot fail; this one aborts with a diagnostic if the device
+ * fails (use ec_method_encode_batch for an error code). */
+void ec_method_encode(ec_matrix_list_t *list, uint64_t size, void *in, void **out);
+
+/* Replaces ec-method.c:410-433 (ec-inode-read.c:1196).  size: bytes per
+ * fragment (multiple of EC_METHOD_CHUNK_SIZE).  mask: the k bricks used;
+ * rows[p] = brick index + 1 of in[p], ascending.  out: size * k bytes.
+ * Returns 0, -EINVAL, -ENOMEM or -EIO. */
+int32_t ec_method_decode(ec_matrix_list_t *list, uint64_t size, uintptr_t mask,
+                         uint32_t *rows, void **in, void *out);
+
+/* ------------------------------------------------------------------------
+ * Batched / device-resident entry points (new).
+ * --------------------------------------------------------------------- */
+
+/* Encode nstripes stripes; in = nstripes*k*512 bytes, out[i] = nstripes*512
+ * bytes.  Host buffers are split by stripe range across all visible MI355X
+ * devices with overlapped PCIe transfers; device buffers run on device 0.
+ * Does not modify out[].  Returns 0 or -errno. */
+int32_t ec_method_encode_batch(ec_matrix_list_t *list, uint64_t nstripes,
+                               const void *in, void *const *out);
+
+/* Decode nstripes stripes with one mask (as ec_method_decode, sizes in
+ * stripes).  Returns 0 or -errno. */
+int32_t ec_method_decode_batch(ec_matrix_list_t *list, uint64_t nstripes,
+                               uintptr_t mask, const uint32_t *rows,
+                               const void *const *in, void *out);
+
+/* Self-heal style reconstruction with mixed erasure patterns: frags[0..n)
+ * are all n fragment buffers (nstripes*512 bytes each; entries of bricks no
+ * group reads may be NULL), group g = stripes [g*group_stripes,
+ * (g+1)*group_stripes) is decoded from the k bricks in group_masks[g].
+ * group_stripes is a power of two >= 8.  out = nstripes*k*512 bytes. */
+int32_t ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes,
+                               uint64_t group_stripes, const uintptr_t *group_masks,
+                               const void *const *frags, void *out);
+
+/* Fused heal: regenerate the fragments of the bricks
+ * in `target_mask` straight from the k fragments in `mask`, without
+ * materialising the decoded data: out[j] (nstripes*512 bytes) is the fragment
+ * of the j-th set bit of target_mask.  Returns 0 or -errno. */
+int32_t ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
+                       const void *const *in, uintptr_t target_mask,
+                       void *const *out);
+
+/* Device-resident, asynchronous variants for callers that keep stripes in
+ * MI355X memory: all buffers are device pointers on `device` (index among
+ * the visible gfx950 devices), work is queued on `stream` (a hipStream_t;
+ * NULL = the calling thread's per-thread default stream) and the call returns
+ * without waiting.  The decode matrix travels in the kernel arguments, so no
+ * host state outlives the call. */
+int32_t ec_method_encode_device(ec_matrix_list_t *list, int device, void *stream,
+                                uint64_t nstripes, const void *in, void *const *out);
+int32_t ec_method_decode_device(ec_matrix_list_t *list, int device, void *stream,
+                                uint64_t nstripes, uintptr_t mask,
+                                const void *const *in, void *out);
+/* group_pattern: device array of nstripes/group_stripes bytes indexing
+ * masks[0..nmasks) (nmasks is limited by the kernel-argument segment). */
+int32_t ec_method_decode_mixed_device(ec_matrix_list_t *list, int device,
+                                      void *stream, uint64_t nstripes,
+                                      uint64_t group_stripes,
+                                      const uint8_t *group_pattern,
+                                      uint32_t nmasks, const uintptr_t *masks,
+                                      const void *const *frags, void *out);
+int32_t ec_method_heal_device(ec_matrix_list_t *list, int device, void *stream,
+                              uint64_t nstripes, uintptr_t mask,
+                              const void *const *in, uintptr_t target_mask,
+                              void *const *out);
+int32_t ec_method_sync_device(int device, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Utilities.
+ * --------------------------------------------------------------------- */
+
+/* Number of visible gfx950 devices (0 = the library cannot run). */
+int32_t ec_method_device_count(void);
+/* Last device-layer error string (diagnostics). */
+const char *ec_method_last_error(void);
+/* Pinned host memory for zero-copy PCIe transfers. */
+void *ec_method_host_alloc(size_t bytes);
+void ec_method_host_free(void *p);
+
+/* Host-side matrix helpers, exported for tests and tools: the n x k encode
+ * matrix (ec-method.c:22-36) and the k x k inverse for ascending rows
+ * (ec-method.c:38-72), as uint32 values in [0, 255].  Return 0 or -EINVAL. */
+int32_t ec_method_encode_matrix(uint32_t columns, uint32_t rows, uint32_t *matrix);
+int32_t ec_method_inverse_matrix(uint32_t columns, const uint32_t *rows,
+                                 uint32_t *matrix);
+uint32_t ec_method_gf_mul(uint32_t a, uint32_t b);
+uint32_t ec_method_gf_div(uint32_t a, uint32_t b);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EC_MI355X_EC_METHOD_H */

@@ -1,0 +1,218 @@
+"""GPU parity: the HIP kernels through the C ABI vs the CPU oracle.
+
+Bit-exact comparison (integer GF(2^8) work: no tolerance).  Small seeded
+inputs go through both the oracle and the library; inputs are host numpy
+buffers (PCIe path) or torch device tensors (device-resident path).
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CHUNK = 512
+
+
+@pytest.fixture(scope="module")
+def ec():
+    import glusterfs_amd as g
+    if g.device_count() < 1:
+        pytest.fail("no MI355X visible: the product has no CPU path")
+    return g
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def rand_bytes(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
+
+
+GEOMS = [(2, 3), (3, 4), (4, 5), (4, 6), (6, 8), (8, 10), (8, 12), (10, 13), (16, 18),
+         (16, 20), (16, 31)]
+
+
+@pytest.mark.parametrize("k,n", GEOMS)
+@pytest.mark.parametrize("nstripes", [1, 7, 64, 133])
+def test_encode_host_matches_oracle(ec, oracle, k, n, nstripes):
+    data = rand_bytes(CHUNK * k * nstripes, seed=k * 1000 + n * 10 + nstripes)
+    want = oracle.encode(k, n, data)
+    with ec.ECMatrixList(k, n) as L:
+        got = [np.full(CHUNK * nstripes, 0xA5, dtype=np.uint8) for _ in range(n)]
+        outs = list(got)
+        L.encode(data.size, data, outs)
+        for i in range(n):
+            assert np.array_equal(got[i], want[i]), "fragment %d" % i
+
+
+@pytest.mark.parametrize("k,n", [(2, 3), (4, 6), (8, 12), (16, 20), (5, 7)])
+def test_encode_device_matches_oracle(ec, oracle, torch_cuda, k, n):
+    torch = torch_cuda
+    nstripes = 1000
+    data = rand_bytes(CHUNK * k * nstripes, seed=11 + k)
+    want = oracle.encode(k, n, data)
+    din = torch.from_numpy(data).cuda()
+    douts = [torch.empty(CHUNK * nstripes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    with ec.ECMatrixList(k, n) as L:
+        L.encode_batch(nstripes, din, douts)  # device pointers -> device path
+        for i in range(n):
+            assert np.array_equal(douts[i].cpu().numpy(), want[i]), "fragment %d" % i
+
+
+def _decode_case(ec, oracle, L, k, n, rows, frags, nstripes, device=False):
+    import torch
+    want = oracle.decode(k, rows, [frags[r - 1] for r in rows])
+    mask = sum(1 << (r - 1) for r in rows)
+    if device:
+        ins = [torch.from_numpy(frags[r - 1]).cuda() for r in rows]
+        out = torch.empty(CHUNK * k * nstripes, dtype=torch.uint8, device="cuda")
+        L.decode_batch(nstripes, mask, rows, ins, out)
+        got = out.cpu().numpy()
+    else:
+        out = np.zeros(CHUNK * k * nstripes, dtype=np.uint8)
+        L.decode(CHUNK * nstripes, mask, rows, [frags[r - 1] for r in rows], out)
+        got = out
+    assert np.array_equal(got, want), rows
+
+
+@pytest.mark.parametrize("k,n", [(2, 3), (3, 4), (4, 6), (8, 12)])
+def test_decode_all_masks_random_fragments(ec, oracle, k, n):
+    """Fragments are random (not codewords): checks the full linear map."""
+    nstripes = 9
+    frags = [rand_bytes(CHUNK * nstripes, seed=100 + i) for i in range(n)]
+    with ec.ECMatrixList(k, n) as L:
+        for rows in itertools.combinations(range(1, n + 1), k):
+            _decode_case(ec, oracle, L, k, n, list(rows), frags, nstripes)
+
+
+@pytest.mark.parametrize("k,n", [(16, 20), (16, 18), (10, 13)])
+def test_decode_sampled_masks(ec, oracle, k, n):
+    nstripes = 17
+    frags = [rand_bytes(CHUNK * nstripes, seed=300 + i) for i in range(n)]
+    combos = list(itertools.combinations(range(1, n + 1), k))
+    rng = np.random.default_rng(5)
+    with ec.ECMatrixList(k, n) as L:
+        for idx in rng.choice(len(combos), size=min(60, len(combos)), replace=False):
+            _decode_case(ec, oracle, L, k, n, list(combos[idx]), frags, nstripes)
+
+
+@pytest.mark.parametrize("k,n", [(4, 6), (8, 12), (16, 20)])
+def test_decode_device_roundtrip(ec, oracle, torch_cuda, k, n):
+    nstripes = 777
+    data = rand_bytes(CHUNK * k * nstripes, seed=3)
+    frags = oracle.encode(k, n, data)
+    with ec.ECMatrixList(k, n) as L:
+        rows = list(range(n - k + 1, n + 1))      # the first r bricks missing
+        _decode_case(ec, oracle, L, k, n, rows, frags, nstripes, device=True)
+        rows = sorted(np.random.default_rng(1).choice(n, k, replace=False) + 1)
+        _decode_case(ec, oracle, L, k, n, [int(r) for r in rows], frags, nstripes, device=True)
+
+
+def test_empty_and_cache(ec, oracle):
+    k, n = 4, 6
+    with ec.ECMatrixList(k, n, max=3) as L:
+        L.encode(0, np.zeros(0, np.uint8), [np.zeros(0, np.uint8)] * n)
+        L.decode(0, 0x0F, [1, 2, 3, 4], [np.zeros(0, np.uint8)] * k, np.zeros(0, np.uint8))
+        frags = [rand_bytes(CHUNK * 3, seed=i) for i in range(n)]
+        for rows in itertools.combinations(range(1, 7), 4):   # 15 masks > cache of 3
+            _decode_case(ec, oracle, L, k, n, list(rows), frags, 3)
+        assert L.count <= 3
+
+
+def test_invalid_arguments(ec):
+    with ec.ECMatrixList(4, 6) as L:
+        buf = np.zeros(CHUNK * 4, np.uint8)
+        with pytest.raises(OSError):   # mask with 3 bits
+            L.decode(CHUNK, 0x07, [1, 2, 3], [buf] * 4, buf)
+        with pytest.raises(OSError):   # rows inconsistent with mask
+            L.decode(CHUNK, 0x0F, [1, 2, 3, 5], [buf] * 4, buf)
+        with pytest.raises(OSError):   # size not a multiple of the chunk
+            L.decode(100, 0x0F, [1, 2, 3, 4], [buf] * 4, buf)
+    with pytest.raises(OSError):
+        ec.ECMatrixList(8, 4)
+    with pytest.raises(OSError):
+        ec.ECMatrixList(17, 20)
+
+
+def test_encode_advances_out_pointers(ec, oracle):
+    """ec-method.c:405: each out[i] is advanced by size/k (ec_method_encode)."""
+    import ctypes
+    k, n, nst = 4, 6, 5
+    data = rand_bytes(CHUNK * k * nst, seed=8)
+    bufs = [np.zeros(CHUNK * nst, np.uint8) for _ in range(n)]
+    with ec.ECMatrixList(k, n) as L:
+        ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+        ec.ec_method.lib.ec_method_encode(ctypes.byref(L._list), data.size, data.ctypes.data,
+                                          ptrs)
+        for i in range(n):
+            assert ptrs[i] == bufs[i].ctypes.data + CHUNK * nst
+    want = oracle.encode(k, n, data)
+    for i in range(n):
+        assert np.array_equal(bufs[i], want[i])
+
+
+@pytest.mark.parametrize("k,n", [(4, 6), (8, 12)])
+def test_decode_mixed_patterns(ec, oracle, k, n):
+    group = 16
+    ngroups = 23
+    nstripes = group * ngroups - 5          # ragged last group
+    data = rand_bytes(CHUNK * k * nstripes, seed=21)
+    frags = oracle.encode(k, n, data)
+    combos = list(itertools.combinations(range(n), k))
+    rng = np.random.default_rng(4)
+    masks = [sum(1 << b for b in combos[i]) for i in rng.choice(len(combos), ngroups)]
+    out = np.zeros(CHUNK * k * nstripes, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed(nstripes, group, masks, frags, out)
+    assert np.array_equal(out, data)
+
+
+@pytest.mark.parametrize("k,n", [(4, 6), (8, 12), (16, 20)])
+def test_heal_regenerates_missing_fragments(ec, oracle, k, n):
+    nstripes = 300
+    data = rand_bytes(CHUNK * k * nstripes, seed=31)
+    frags = oracle.encode(k, n, data)
+    rows = list(range(n - k + 1, n + 1))               # good bricks: the last k
+    mask = sum(1 << (r - 1) for r in rows)
+    target = ((1 << n) - 1) & ~mask                     # regenerate the rest
+    tgt = [i for i in range(n) if (target >> i) & 1]
+    outs = [np.zeros(CHUNK * nstripes, np.uint8) for _ in tgt]
+    with ec.ECMatrixList(k, n) as L:
+        L.heal(nstripes, mask, [frags[r - 1] for r in rows], target, outs)
+    for o, i in zip(outs, tgt):
+        assert np.array_equal(o, frags[i]), "brick %d" % i
+
+
+def test_concurrent_callers(ec, oracle):
+    """Re-entrancy: many threads share one list (ec-method.c:206,250 lock)."""
+    import threading
+    k, n, nst = 4, 6, 40
+    data = rand_bytes(CHUNK * k * nst, seed=77)
+    frags = oracle.encode(k, n, data)
+    errors = []
+    with ec.ECMatrixList(k, n) as L:
+        def worker(t):
+            try:
+                for rows in list(itertools.combinations(range(1, 7), 4))[t::4]:
+                    out = np.zeros(data.size, np.uint8)
+                    mask = sum(1 << (r - 1) for r in rows)
+                    L.decode(CHUNK * nst, mask, list(rows), [frags[r - 1] for r in rows], out)
+                    if not np.array_equal(out, data):
+                        errors.append(rows)
+                    enc = [np.zeros(CHUNK * nst, np.uint8) for _ in range(n)]
+                    L.encode_batch(nst, data, enc)
+                    if any(not np.array_equal(a, b) for a, b in zip(enc, frags)):
+                        errors.append(("enc", t))
+            except Exception as e:  # pragma: no cover
+                errors.append(repr(e))
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    assert not errors
