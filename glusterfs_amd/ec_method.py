@@ -60,6 +60,15 @@ assert ctypes.sizeof(MatrixList) == 120
 
 
 def _load():
+    # One HIP runtime per process: the torch wheel bundles its own
+    # libamdhip64.so.7, and libc10_hip links it by a different name, so if
+    # this library were loaded first the process would end up with two HIP
+    # runtimes (torch then reports no GPU).  Importing torch first makes the
+    # dynamic loader bind our libamdhip64.so.7 dependency to torch's copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             "libec_mi355x.so not built (%s); run `make -C glusterfs_amd` or "
