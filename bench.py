@@ -3,22 +3,24 @@
 
 One "step" = one pass of the hot path over one batch resident in HBM:
 decoding 1 GiB of user data of a disperse 4+2 volume with 2 fragments
-missing (mask 0x3C: bricks 0 and 1 lost), i.e. BASELINE.json configs[1].
+missing (mask 0x3C: bricks 0 and 1 lost) -- BASELINE.json configs[1].
 With --gpus N (one process per GPU under torch.distributed.run) every rank
-decodes its own 1 GiB stripe range (weak scaling; stripes are independent,
-no collective touches the data path -- the only collectives are the barrier
-and the max-over-ranks of the timing).
+decodes its own 1 GiB stripe range of an N GiB job (weak scaling): stripes
+are independent, so no collective touches the data path; the only
+collectives are the barrier around the timed region, the max over ranks of
+the elapsed time and an all-ranks parity flag (glusterfs_amd/dist.py).
 
-Besides the headline line, the JSON carries:
-  roofline      HBM roofline of the decode kernel (algorithmic bytes 2*S per
-                launch / average launch time measured with HIP events on the
-                launch stream; traffic from the committed rocprofv3 PMC run)
-  cpu_baseline  the CPU oracle (oracle/, a C restatement of the reference
+The JSON line also carries
+  roofline      the decode kernel against the 8 TB/s HBM peak: algorithmic
+                bytes per launch (2*S: read k fragments = S, write S) over the
+                average launch time measured with HIP events on the launch
+                stream; `traffic` = PMC-measured HBM bytes per launch from the
+                committed rocprofv3 run (profiles/traffic.json)
+  cpu_baseline  the CPU oracle (oracle/, C restatement of the reference
                 algorithm) decoding a bounded sample of the same fragments on
-                the host's cores, rank 0 at N=1 only
-  extra         the other BASELINE configs measured the same way (4+2 and
-                8+4 encode/decode device-resident, 16+4 encode, mixed-pattern
-                self-heal decode, PCIe-inclusive end-to-end rates)
+                16 host threads, rank 0 at N=1 only
+  extra         (N=1) the other BASELINE configs measured the same way, a
+                copy calibration, and PCIe-inclusive end-to-end rates
 """
 import argparse
 import json
@@ -40,10 +42,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gib", type=float, default=1.0, help="user data per GPU per step")
-    ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--extra", dest="extra", action="store_true", default=None)
+    ap.add_argument("--no-extra", dest="extra", action="store_false")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--only", default=None, help="profile helper: run one config only")
+    ap.add_argument("--only", default=None,
+                    help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R | heal:K+R")
     return ap.parse_args()
+
+
+def gbps(nbytes, seconds):
+    return nbytes / seconds / 1e9
 
 
 def rand_u8(torch, nbytes, seed, device):
@@ -54,105 +62,197 @@ def rand_u8(torch, nbytes, seed, device):
     return x.view(torch.uint8)
 
 
-class Timer:
-    """K launches between two HIP events on the launch stream."""
+def timed(torch, fn, steps, warmup, group=None):
+    """Warmup, then exactly `steps` launches between two HIP events on the
+    launch stream, bracketed by barrier + synchronize."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if group:
+        group.barrier()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        fn()
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if group:
+        group.barrier()
+    return wall, ev0.elapsed_time(ev1) / 1e3 / steps
 
-    def __init__(self, torch):
-        self.torch = torch
 
-    def run(self, fn, steps, warmup, barrier=None):
+class Ctx:
+    def __init__(self, g, torch, dev):
+        self.g, self.torch, self.dev = g, torch, dev
+        self.sp = torch.cuda.current_stream(dev).cuda_stream
+
+    def encoded(self, k, n, nbytes, seed):
         torch = self.torch
-        for _ in range(warmup):
-            fn()
-        torch.cuda.synchronize()
-        if barrier:
-            barrier()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record()
-        for _ in range(steps):
-            fn()
-        ev1.record()
-        torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
-        if barrier:
-            barrier()
-        return wall, ev0.elapsed_time(ev1) / 1e3
+        nst = nbytes // (CHUNK * k)
+        data = rand_u8(torch, nst * CHUNK * k, seed, self.dev)
+        frags = [torch.empty(nst * CHUNK, dtype=torch.uint8, device=self.dev) for _ in range(n)]
+        L = self.g.ECMatrixList(k, n)
+        L.encode_device(self.dev.index, self.sp, nst, data, frags)
+        return L, data, frags, nst
 
 
-def measure_decode(g, torch, dev, stream, k, n, nbytes, mask, steps, warmup, seed,
-                   barrier=None):
-    nst = nbytes // (CHUNK * k)
-    data = rand_u8(torch, nst * CHUNK * k, seed, dev)
-    frags = [torch.empty(nst * CHUNK, dtype=torch.uint8, device=dev) for _ in range(n)]
-    L = g.ECMatrixList(k, n)
-    sp = stream.cuda_stream
-    L.encode_device(dev.index, sp, nst, data, frags)
-    rows = g.mask_rows(mask)
+def run_decode(c, k, n, nbytes, mask, steps, warmup, seed, group=None):
+    L, data, frags, nst = c.encoded(k, n, nbytes, seed)
+    rows = c.g.mask_rows(mask)
     ins = [frags[r - 1] for r in rows]
-    out = torch.empty_like(data)
-    wall, ev = Timer(torch).run(lambda: L.decode_device(dev.index, sp, nst, mask, ins, out),
-                                steps, warmup, barrier)
-    ok = bool(torch.equal(out, data))
-    return dict(L=L, data=data, frags=frags, out=out, rows=rows, nst=nst, wall=wall,
-                kernel_s=ev / steps, ok=ok, user_bytes=nst * CHUNK * k)
+    out = c.torch.empty_like(data)
+    wall, kt = timed(c.torch, lambda: L.decode_device(c.dev.index, c.sp, nst, mask, ins, out),
+                     steps, warmup, group)
+    ok = bool(c.torch.equal(out, data))
+    return dict(wall=wall, kernel_s=kt, ok=ok, user=nst * CHUNK * k, nst=nst, frags=frags,
+                rows=rows)
 
 
-def measure_encode(g, torch, dev, stream, k, n, nbytes, steps, warmup, seed):
-    nst = nbytes // (CHUNK * k)
-    data = rand_u8(torch, nst * CHUNK * k, seed, dev)
-    frags = [torch.empty(nst * CHUNK, dtype=torch.uint8, device=dev) for _ in range(n)]
-    L = g.ECMatrixList(k, n)
-    sp = stream.cuda_stream
-    wall, ev = Timer(torch).run(lambda: L.encode_device(dev.index, sp, nst, data, frags),
-                                steps, warmup)
-    # parity spot check: decode from the last k bricks must return the data
+def run_encode(c, k, n, nbytes, steps, warmup, seed):
+    torch = c.torch
+    L, data, frags, nst = c.encoded(k, n, nbytes, seed)
+    wall, kt = timed(torch, lambda: L.encode_device(c.dev.index, c.sp, nst, data, frags),
+                     steps, warmup)
     rows = list(range(n - k + 1, n + 1))
     out = torch.empty_like(data)
-    L.decode_device(dev.index, sp, nst, sum(1 << (r - 1) for r in rows),
+    L.decode_device(c.dev.index, c.sp, nst, sum(1 << (r - 1) for r in rows),
                     [frags[r - 1] for r in rows], out)
     torch.cuda.synchronize()
-    ok = bool(torch.equal(out, data))
-    return dict(kernel_s=ev / steps, wall=wall, ok=ok, user_bytes=nst * CHUNK * k)
+    return dict(kernel_s=kt, ok=bool(torch.equal(out, data)), user=nst * CHUNK * k)
 
 
-def gbps(nbytes, seconds):
-    return nbytes / seconds / 1e9
+def run_mixed(c, k, n, nbytes, steps, warmup, seed, group_stripes=1024, nmasks=16):
+    """Self-heal reconstruct (configs[4]): every 1024-stripe group is decoded
+    from its own k-of-n brick set, drawn (seeded) from `nmasks` masks."""
+    import random
+    torch = c.torch
+    L, data, frags, nst = c.encoded(k, n, nbytes, seed)
+    rnd = random.Random(seed)
+    masks = []
+    while len(masks) < nmasks:
+        m = sum(1 << b for b in rnd.sample(range(n), k))
+        if m not in masks:
+            masks.append(m)
+    ngroups = (nst + group_stripes - 1) // group_stripes
+    gp = torch.tensor([rnd.randrange(nmasks) for _ in range(ngroups)], dtype=torch.uint8,
+                      device=c.dev)
+    out = torch.empty_like(data)
+    wall, kt = timed(torch, lambda: L.decode_mixed_device(c.dev.index, c.sp, nst, group_stripes,
+                                                          gp, masks, frags, out), steps, warmup)
+    return dict(kernel_s=kt, ok=bool(torch.equal(out, data)), user=nst * CHUNK * k)
 
 
-def extra_configs(g, torch, dev, stream, steps, warmup):
-    ex = {}
+def run_heal(c, k, n, nbytes, steps, warmup, seed):
+    """Fused heal: regenerate the r lost fragments
+    directly from k good ones (reads S, writes r*S/k)."""
+    torch = c.torch
+    L, data, frags, nst = c.encoded(k, n, nbytes, seed)
+    good = list(range(n - k, n))                 # bricks 0..r-1 lost
+    mask = sum(1 << b for b in good)
+    target = ((1 << n) - 1) & ~mask
+    outs = [torch.empty(nst * CHUNK, dtype=torch.uint8, device=c.dev) for _ in range(n - k)]
+    ins = [frags[b] for b in good]
+    wall, kt = timed(torch, lambda: L.heal_device(c.dev.index, c.sp, nst, mask, ins, target,
+                                                  outs), steps, warmup)
+    ok = all(torch.equal(o, frags[i]) for i, o in enumerate(outs))
+    return dict(kernel_s=kt, ok=ok, user=nst * CHUNK * k, alg=nst * CHUNK * (k + n - k))
+
+
+def run_e2e(c, k, n, nbytes, steps):
+    """PCIe-inclusive: pinned host buffers in, pinned host buffers out, the
+    library's pipelined H2D / kernel / D2H path (all visible GPUs)."""
+    import ctypes
+    import numpy as np
+    g = c.g
+    nst = nbytes // (CHUNK * k)
+    S = nst * CHUNK * k
+    lib = g.ec_method.lib
+
+    def pinned(nb):
+        p = lib.ec_method_host_alloc(nb)
+        if not p:
+            raise MemoryError
+        return p, np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(p))
+
+    res = {}
+    bufs = []
+    try:
+        din_p, din = pinned(S)
+        bufs.append(din_p)
+        din[:] = rand_u8(c.torch, S, 99, c.dev).cpu().numpy()
+        fr = [pinned(nst * CHUNK) for _ in range(n)]
+        bufs += [p for p, _ in fr]
+        dout_p, dout = pinned(S)
+        bufs.append(dout_p)
+        with g.ECMatrixList(k, n) as L:
+            L.encode_batch(nst, din_p, [p for p, _ in fr])          # warm
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                L.encode_batch(nst, din_p, [p for p, _ in fr])
+            te = (time.perf_counter() - t0) / steps
+            rows = list(range(n - k + 1, n + 1))
+            mask = sum(1 << (r - 1) for r in rows)
+            ins = [fr[r - 1][0] for r in rows]
+            L.decode_batch(nst, mask, rows, ins, dout_p)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                L.decode_batch(nst, mask, rows, ins, dout_p)
+            td = (time.perf_counter() - t0) / steps
+            ok = bool(np.array_equal(dout, din))
+        res = dict(enc_user_GBps=round(gbps(S, te), 2), dec_user_GBps=round(gbps(S, td), 2),
+                   ok=ok, bytes=S, buffers="pinned host (ec_method_host_alloc)")
+    finally:
+        for p in bufs:
+            lib.ec_method_host_free(p)
+    return res
+
+
+def copy_calibration(torch, dev, steps):
+    """Device-to-device copy of 1 GiB with torch's kernel (context only)."""
+    a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    _, kt = timed(torch, lambda: b.copy_(a), steps, 2)
+    del a, b
+    return round(gbps(2 << 30, kt), 1)
+
+
+def frac(nbytes, seconds):
+    return round(gbps(nbytes, seconds) / HBM_PEAK_GBPS, 4)
+
+
+def extra_configs(c, steps, warmup):
+    torch = c.torch
     st = max(3, steps // 2)
-    # 4+2 encode, 1 GiB
-    r = measure_encode(g, torch, dev, stream, 4, 6, 1 << 30, st, warmup, 11)
-    ex["enc_4+2_1GiB"] = dict(user_GBps=round(gbps(r["user_bytes"], r["kernel_s"]), 1),
-                              hbm_frac=round(gbps(2.5 * r["user_bytes"], r["kernel_s"]) /
-                                             HBM_PEAK_GBPS, 4), ok=r["ok"])
-    # 8+4, 64K-stripe batches (256 MiB user)
-    nb = 65536 * CHUNK * 8
-    r = measure_encode(g, torch, dev, stream, 8, 12, nb, st, warmup, 12)
-    ex["enc_8+4_64Kstripes"] = dict(user_GBps=round(gbps(r["user_bytes"], r["kernel_s"]), 1),
-                                    hbm_frac=round(gbps(2.5 * r["user_bytes"], r["kernel_s"]) /
-                                                   HBM_PEAK_GBPS, 4), ok=r["ok"])
-    for name, mask in (("dec_8+4_0xFF0", 0xFF0), ("dec_8+4_0xEB5", 0xEB5)):
-        r = measure_decode(g, torch, dev, stream, 8, 12, nb, mask, st, warmup, 13)
-        ex[name] = dict(user_GBps=round(gbps(r["user_bytes"], r["kernel_s"]), 1),
-                        hbm_frac=round(gbps(2 * r["user_bytes"], r["kernel_s"]) /
-                                       HBM_PEAK_GBPS, 4), ok=r["ok"])
-        del r
-    # 4+2 decode, bricks 4 and 5 lost
-    r = measure_decode(g, torch, dev, stream, 4, 6, 1 << 30, 0x0F, st, warmup, 14)
-    ex["dec_4+2_0x0F"] = dict(user_GBps=round(gbps(r["user_bytes"], r["kernel_s"]), 1),
-                              hbm_frac=round(gbps(2 * r["user_bytes"], r["kernel_s"]) /
-                                             HBM_PEAK_GBPS, 4), ok=r["ok"])
-    del r
-    # 16+4 encode, 2 GiB per GPU
-    r = measure_encode(g, torch, dev, stream, 16, 20, 2 << 30, st, warmup, 15)
-    ex["enc_16+4_2GiB"] = dict(user_GBps=round(gbps(r["user_bytes"], r["kernel_s"]), 1),
-                               hbm_frac=round(gbps(2.25 * r["user_bytes"], r["kernel_s"]) /
-                                              HBM_PEAK_GBPS, 4), ok=r["ok"])
+    ex = {"copy_calibration_GBps": copy_calibration(torch, c.dev, st)}
+
+    def put(name, r, alg):
+        ex[name] = dict(user_GBps=round(gbps(r["user"], r["kernel_s"]), 1),
+                        hbm_frac=frac(alg, r["kernel_s"]), ok=r["ok"])
+
+    r = run_encode(c, 4, 6, 1 << 30, st, warmup, 11)
+    put("enc_4+2_1GiB", r, 2.5 * r["user"])
+    r = run_decode(c, 4, 6, 1 << 30, 0x0F, st, warmup, 14)
+    put("dec_4+2_0x0F_1GiB", r, 2 * r["user"])
+    nb = 65536 * CHUNK * 8                       # configs[2]: 64K-stripe batches
+    r = run_encode(c, 8, 12, nb, st, warmup, 12)
+    put("enc_8+4_64Kstripes", r, 2.5 * r["user"])
+    for name, mask in (("dec_8+4_0xFF0_64Kstripes", 0xFF0),
+                       ("dec_8+4_0xEB5_64Kstripes", 0xEB5)):
+        r = run_decode(c, 8, 12, nb, mask, st, warmup, 13)
+        put(name, r, 2 * r["user"])
+    r = run_decode(c, 8, 12, 1 << 30, 0xFF0, st, warmup, 16)
+    put("dec_8+4_0xFF0_1GiB", r, 2 * r["user"])
+    r = run_encode(c, 16, 20, 2 << 30, st, warmup, 15)
+    put("enc_16+4_2GiB", r, 2.25 * r["user"])
+    r = run_mixed(c, 8, 12, 1 << 30, st, warmup, 17)
+    put("selfheal_mixed16_8+4_1GiB", r, 2 * r["user"])
+    r = run_heal(c, 8, 12, 1 << 30, st, warmup, 18)
+    put("heal_fused_8+4_regen4_1GiB", r, r["alg"])
     torch.cuda.empty_cache()
+    ex["e2e_pcie_4+2_512MiB"] = run_e2e(c, 4, 6, 512 << 20, 3)
     return ex
 
 
@@ -177,65 +277,57 @@ def cpu_baseline(sample_frags, rows, k, budget_s=10.0):
                        (user >> 20, passes, threads))
 
 
+def only(c, spec, nbytes, steps, warmup):
+    parts = spec.split(":")
+    k, r = map(int, parts[1].split("+"))
+    n = k + r
+    if parts[0] == "enc":
+        res = run_encode(c, k, n, nbytes, steps, warmup, 1)
+    elif parts[0] == "dec":
+        res = run_decode(c, k, n, nbytes, int(parts[2], 16), steps, warmup, 1)
+    elif parts[0] == "mixed":
+        res = run_mixed(c, k, n, nbytes, steps, warmup, 1)
+    else:
+        res = run_heal(c, k, n, nbytes, steps, warmup, 1)
+    print(json.dumps(dict(only=spec, kernel_ms=res["kernel_s"] * 1e3, ok=res["ok"])))
+
+
 def main():
     args = parse()
     import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
-    barrier = (lambda: dist.barrier()) if world > 1 else None
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
     import glusterfs_amd as g
+    from glusterfs_amd.dist import Group
+
+    grp = Group()
+    torch.cuda.set_device(grp.local)
+    dev = torch.device("cuda", grp.local)
+    c = Ctx(g, torch, dev)
+    nbytes = int(args.gib * (1 << 30))
+    if args.only:
+        return only(c, args.only, nbytes, args.steps, args.warmup)
 
     k, n, mask = 4, 6, 0x3C
-    nbytes = int(args.gib * (1 << 30)) // (CHUNK * k) * (CHUNK * k)
-    if args.only:
-        # profiling helper (rocprofv3): one config, steps launches, no extras
-        k2, n2 = map(int, args.only.split(":")[1].split("+"))
-        n2 += k2
-        if args.only.startswith("enc"):
-            r = measure_encode(g, torch, dev, stream, k2, n2, nbytes, args.steps, args.warmup, 1)
-        else:
-            m = int(args.only.split(":")[2], 16)
-            r = measure_decode(g, torch, dev, stream, k2, n2, nbytes, m, args.steps,
-                               args.warmup, 1)
-        print(json.dumps(dict(only=args.only, kernel_ms=r["kernel_s"] * 1e3, ok=r["ok"])))
-        return
-
-    r = measure_decode(g, torch, dev, stream, k, n, nbytes, mask, args.steps, args.warmup,
-                       1234 + rank, barrier)
-    wall = r["wall"]
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-        okt = torch.tensor([1 if r["ok"] else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        r["ok"] = bool(okt.item())
-    user_total = r["user_bytes"] * world * args.steps
-    value = gbps(user_total, wall)
-    kernel_s = r["kernel_s"]
-    achieved = gbps(2 * r["user_bytes"], kernel_s)
+    r = run_decode(c, k, n, nbytes, mask, args.steps, args.warmup, 1234 + grp.rank, grp)
+    wall = grp.max(r["wall"])
+    ok = grp.all_ok(r["ok"])
+    value = gbps(r["user"] * grp.world * args.steps, wall)
+    kt = r["kernel_s"]
+    achieved = gbps(2 * r["user"], kt)
 
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get("dec_4+2_0x3C_1GiB", {}).get("hbm_bytes_per_launch")
-        except Exception:
+            traffic = json.load(open(tf)).get("dec_4+2_0x3C_1GiB", {}).get(
+                "hbm_bytes_per_launch")
+        except (OSError, ValueError):
             traffic = None
 
     out = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "GB/s",
-        "n_gpus": world,
+        "n_gpus": grp.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(wall / args.steps * 1e3, 4),
@@ -247,11 +339,12 @@ def main():
         "config": {
             "workload": "disperse 4+2 decode, 2 fragments missing (mask 0x3C), "
                         "%d MiB user data per GPU per step (BASELINE configs[1])" %
-                        (r["user_bytes"] >> 20),
+                        (r["user"] >> 20),
             "k": k, "n": n, "mask": "0x3C", "stripes_per_gpu": r["nst"],
-            "parallelism": "stripe-range partition, %d GPU(s), no collective" % world,
+            "parallelism": "stripe-range partition over %d GPU(s), no data collective" %
+                           grp.world,
         },
-        "parity_ok": r["ok"],
+        "parity_ok": ok,
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -259,28 +352,26 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": "ec_combine<4,false> (decode)",
-            "algorithmic_bytes_per_launch": 2 * r["user_bytes"],
-            "avg_launch_ms": round(kernel_s * 1e3, 4),
+            "kernel": "ec_combine<4,2,false,false,false> (decode)",
+            "algorithmic_bytes_per_launch": 2 * r["user"],
+            "avg_launch_ms": round(kt * 1e3, 4),
         },
     }
     frags_host = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        sample = 128 << 20  # user bytes in the CPU sample
-        fs = sample // k
+    if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
+        fs = (128 << 20) // k                  # 128 MiB of user data
         frags_host = [r["frags"][x - 1][:fs].cpu().numpy() for x in r["rows"]]
     del r
     torch.cuda.empty_cache()
-    if not args.no_extra:
-        out["extra"] = extra_configs(g, torch, dev, stream, args.steps, args.warmup)
+    extra = args.extra if args.extra is not None else grp.world == 1
+    if extra:
+        out["extra"] = extra_configs(c, args.steps, args.warmup)
     if frags_host is not None:
         out["cpu_baseline"] = cpu_baseline(frags_host, [3, 4, 5, 6], k)
-    if world > 1:
-        dist.barrier()
-    if rank == 0:
+    grp.barrier()
+    if grp.rank == 0:
         print(json.dumps(out))
-    if world > 1:
-        dist.destroy_process_group()
+    grp.close()
 
 
 if __name__ == "__main__":

@@ -12,4 +12,9 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                        const void *in, void *const *out);
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d);
 
+namespace ecdev {
+struct CombineArgs;
+}
+int ecdk_pack_args(const ecd_combine_desc_t *d, ecdev::CombineArgs *a);
+
 #endif

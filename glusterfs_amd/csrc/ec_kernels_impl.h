@@ -1,0 +1,342 @@
+/*
+ * ec_kernels_impl.h -- gfx950 kernel templates of the disperse coding path.
+ * Included by ec_kernels.hip (the product launchers) and by the development
+ * harness tools/kbench/kbench.hip, so tuning measures the shipped code.
+ *
+ * Two kernels, both working directly on ec's bit-sliced chunk layout
+ * (512-byte chunks = 8 planes x 64 bytes, ec-method.h:27-29):
+ *
+ *  ec_encode_vander<K, N, W, NTS>   reference: ec_method_encode
+ *      (ec-method.c:394-408) with the per-row Horner kernels ec_code_c_linear
+ *      (ec-code-c.c:11647).  Fragment i of stripe t = Horner over the k data
+ *      chunks with the row's evaluation point v = i + 1 (ec-method.c:22-36,
+ *      284-286).  K, N and therefore every v are compile-time constants, so
+ *      each Horner step is a straight-line XOR tree (ec_gf8.h) -- the gfx950
+ *      counterpart of the reference's JIT'ed row routines (ec-code.c:722).
+ *      A lane owns W dwords of all 8 planes of one chunk column (L = 16/W
+ *      lanes per chunk); its k input chunks stay in VGPRs, so HBM is read once.
+ *
+ *  ec_combine<K, TS, MIXED, NTS>    reference: ec_method_decode
+ *      (ec-method.c:411-433) with ec_code_c_interleaved (ec-code-c.c:11660).
+ *      Output row r of stripe t = XOR_p coef[r][p] * input_p(t) for a run-time
+ *      coefficient matrix held in the kernel-argument segment (constant
+ *      memory, scalar loads).  One block = one tile of T = 8*TS stripes: the
+ *      k input chunks of the tile are staged through LDS with coalesced
+ *      16-byte loads, then each wave computes whole output rows (8 stripes x
+ *      8 lanes x 2 dwords per plane) walking the inputs with a run-time index
+ *      so a single multiply dispatch serves every coefficient: the
+ *      wave-uniform coefficient selects one of 255 compile-time XOR trees
+ *      through a scalar compare tree, zero coefficients are skipped.  MIXED
+ *      picks a pattern (erasure mask -> sources + inverse) per stripe group.
+ *
+ * Tuning knobs measured with tools/kbench (profiles/kbench_*.log): one tile
+ * per block beats a persistent grid with register prefetch (vmcnt also counts
+ * the stores of the previous tile, which serialises the prefetch), and
+ * non-temporal loads lose; NTS (non-temporal stores) is kept as a knob.
+ */
+#ifndef EC_MI355X_KERNELS_IMPL_H
+#define EC_MI355X_KERNELS_IMPL_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "ec_device.h"
+#include "ec_gf8.h"
+
+namespace ecdev {
+
+using ecgf::u32;
+typedef u32 v2u __attribute__((ext_vector_type(2)));
+typedef u32 v4u __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;
+
+template <int W>
+__device__ __forceinline__ void load_plane(const uint8_t *p, u32 (&d)[W])
+{
+    if constexpr (W == 1) {
+        d[0] = *reinterpret_cast<const u32 *>(p);
+    } else if constexpr (W == 2) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(p);
+        d[0] = v.x;
+        d[1] = v.y;
+    } else {
+        const uint4 v = *reinterpret_cast<const uint4 *>(p);
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+    }
+}
+
+template <int W, bool NT>
+__device__ __forceinline__ void store_plane(uint8_t *p, const u32 (&d)[W])
+{
+    if constexpr (NT) {
+        if constexpr (W == 1) {
+            __builtin_nontemporal_store(d[0], reinterpret_cast<u32 *>(p));
+        } else if constexpr (W == 2) {
+            const v2u v = {d[0], d[1]};
+            __builtin_nontemporal_store(v, reinterpret_cast<v2u *>(p));
+        } else {
+            const v4u v = {d[0], d[1], d[2], d[3]};
+            __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
+        }
+    } else {
+        if constexpr (W == 1)
+            *reinterpret_cast<u32 *>(p) = d[0];
+        else if constexpr (W == 2)
+            *reinterpret_cast<uint2 *>(p) = make_uint2(d[0], d[1]);
+        else
+            *reinterpret_cast<uint4 *>(p) = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void load_chunk(const uint8_t *p, u32 (&d)[8][W])
+{
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+        load_plane<W>(p + b * 64, d[b]);
+}
+
+template <int W, bool NT>
+__device__ __forceinline__ void store_chunk(uint8_t *p, const u32 (&d)[8][W])
+{
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+        store_plane<W, NT>(p + b * 64, d[b]);
+}
+
+/* ------------------------------------------------ specialised encoder */
+
+struct FragPtrs {
+    uint8_t *p[ECD_MAX_ROWS];
+};
+
+/* Row I (evaluation point v = I + 1) of the reversed Vandermonde matrix. */
+template <int K, int W, int I, bool NTS>
+__device__ __forceinline__ void encode_row(const u32 (&x)[K][8][W], uint8_t *dst)
+{
+    constexpr u32 v = I + 1;
+    u32 acc[8][W];
+    if constexpr (v == 1) {
+        /* row 0 = XOR of all data chunks, as XOR3 chains */
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                u32 t = x[0][b][w];
+                int j = 1;
+#pragma unroll
+                for (; j + 1 < K; j += 2)
+                    t = ecgf::xor3(t, x[j][b][w], x[j + 1][b][w]);
+                if (j < K)
+                    t ^= x[j][b][w];
+                acc[b][w] = t;
+            }
+    } else {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+                acc[b][w] = x[0][b][w];
+#pragma unroll
+        for (int j = 1; j < K; ++j)
+            ecgf::horner<v, W>(acc, x[j]);
+    }
+    store_chunk<W, NTS>(dst, acc);
+}
+
+template <int K, int W, bool NTS, int... I>
+__device__ __forceinline__ void encode_rows(std::integer_sequence<int, I...>,
+                                            const u32 (&x)[K][8][W], const FragPtrs &out,
+                                            uint64_t off)
+{
+    (encode_row<K, W, I, NTS>(x, out.p[I] + off), ...);
+}
+
+template <int K, int N, int W, bool NTS>
+__global__ __launch_bounds__(kBlock) void ec_encode_vander(const uint8_t *__restrict__ in,
+                                                           const FragPtrs out,
+                                                           uint64_t nstripes)
+{
+    constexpr int L = 16 / W;
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t stripe = gtid / L;
+    if (stripe >= nstripes)
+        return;
+    const u32 colb = (u32)(gtid % L) * (4 * W);
+
+    u32 x[K][8][W];
+    const uint8_t *s = in + stripe * (uint64_t)(K * ECD_CHUNK) + colb;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        load_chunk<W>(s + j * ECD_CHUNK, x[j]);
+
+    encode_rows<K, W, NTS>(std::make_integer_sequence<int, N>{}, x, out,
+                           stripe * (uint64_t)ECD_CHUNK + colb);
+}
+
+template <int W>
+inline uint64_t vander_grid(uint64_t nstripes)
+{
+    return (nstripes * (16 / W) + kBlock - 1) / kBlock;
+}
+
+/* ------------------------------------------------- generic combination */
+
+constexpr int kPatWords = 512; /* kernel-argument pattern space (2 KiB) */
+
+/* Kernel arguments: ecd_combine_desc_t with the patterns re-laid out in
+ * 32-bit words (src[] then one word-aligned row per output, ceil(k/4) words
+ * each) so every coefficient is fetched by a scalar s_load_dword -- a byte
+ * load from the argument segment would be a vector load followed by a
+ * vmcnt(0) wait that also drains all outstanding stores. */
+struct CombineArgs {
+    const uint8_t *in_base[ECD_MAX_ROWS];
+    uint8_t *out_base[ECD_MAX_ROWS];
+    uint64_t in_stride, out_stride, nstripes;
+    const uint8_t *group_pattern;
+    u32 k, kw, rows, group_shift, pwords;
+    u32 pat[kPatWords];
+};
+
+/* LDS byte offset of 16-byte piece q (0..31) of the chunk of input p, tile
+ * stripe s, tile of T stripes.  Plane slots are XOR-rotated by s&3 so the 4
+ * stripes a half wave reads with ds_read_b64 hit 4 different 64-byte bank
+ * windows (conflict-free), and a ds_write_b128 group of 8 lanes (2 planes of
+ * one chunk) covers one full 128-byte bank row. */
+__device__ __forceinline__ u32 lds_piece(u32 p, u32 s, u32 q, u32 T)
+{
+    return (p * T + s) * ECD_CHUNK + ((((q >> 2) ^ (s & 3u)) << 6) | ((q & 3u) << 4));
+}
+
+__device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
+{
+    const u32 w = a.pat[word + (idx >> 2)];
+    return __builtin_amdgcn_readfirstlane((w >> ((idx & 3u) * 8u)) & 0xFFu);
+}
+
+template <int K, int TS, bool MIXED, bool NTS, bool OST>
+__global__ __launch_bounds__(kBlock) void ec_combine(const CombineArgs a)
+{
+    constexpr u32 T = 8 * TS; /* stripes per tile */
+    constexpr int CW = 2;     /* dwords per plane per lane in the compute */
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    uint8_t *const otile = lds + (size_t)k * T * ECD_CHUNK; /* OST: output tile */
+
+    u32 pb = 0;
+    if constexpr (MIXED)
+        pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
+
+    /* stage: 256 threads load 16-byte pieces (32 per chunk), coalesced */
+    {
+        const u32 ls = tid >> 5, lq = tid & 31u;
+        uint4 v[K][TS];
+#pragma unroll
+        for (int p = 0; p < K; ++p) {
+            const u32 src = (u32)p < k ? pat_byte(a, pb, (u32)p) : 0u;
+#pragma unroll
+            for (int j = 0; j < TS; ++j) {
+                const uint64_t st = t0 + ls + 8u * j;
+                v[p][j] = make_uint4(0, 0, 0, 0);
+                if ((u32)p < k && st < a.nstripes)
+                    v[p][j] = *reinterpret_cast<const uint4 *>(a.in_base[src] +
+                                                               st * a.in_stride + lq * 16u);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < K; ++p)
+#pragma unroll
+            for (int j = 0; j < TS; ++j)
+                if ((u32)p < k)
+                    *reinterpret_cast<uint4 *>(lds + lds_piece(p, ls + 8u * j, lq, T)) = v[p][j];
+    }
+    __syncthreads();
+
+    /* compute: (row, 8-stripe subtile) items spread over the 4 waves */
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u, cs = lane >> 3, cc = lane & 7u;
+    const u32 items = a.rows * TS;
+    for (u32 it = wave; it < items; it += kBlock / 64) {
+        const u32 r = it / TS, s = (it % TS) * 8u + cs;
+        u32 acc[8][CW];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int w = 0; w < CW; ++w)
+                acc[b][w] = 0;
+        const u32 rw = pb + a.kw * (1 + r);
+        for (u32 p = 0; p < k; ++p) {
+            const u32 c = pat_byte(a, rw, p);
+            if (c == 0)
+                continue;
+            u32 y[8][CW];
+            const uint8_t *src = lds + (p * T + s) * ECD_CHUNK + cc * 8u;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint2 t = *reinterpret_cast<const uint2 *>(src + (((u32)b ^ (s & 3u)) << 6));
+                y[b][0] = t.x;
+                y[b][1] = t.y;
+            }
+            ecgf::mul_xor_rt<CW>(c, acc, y);
+        }
+        if constexpr (OST) {
+            uint8_t *dst = otile + (r * T + s) * ECD_CHUNK + cc * 8u;
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                *reinterpret_cast<uint2 *>(dst + (((u32)b ^ (s & 3u)) << 6)) =
+                    make_uint2(acc[b][0], acc[b][1]);
+        } else {
+            const uint64_t ost = t0 + s;
+            if (ost < a.nstripes)
+                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+        }
+    }
+    if constexpr (OST) {
+        /* write the output tile back in 16-byte pieces ordered (stripe, row,
+         * piece): decode output (stripe-major) becomes one contiguous run,
+         * per-row outputs (heal, encode) contiguous 512-byte runs */
+        __syncthreads();
+        const u32 npieces = T * a.rows * (ECD_CHUNK / 16);
+        for (u32 e = tid; e < npieces; e += kBlock) {
+            const u32 q = e & 31u, cr = e >> 5;
+            const u32 s = cr / a.rows, r = cr % a.rows;
+            const uint64_t ost = t0 + s;
+            const uint4 v = *reinterpret_cast<const uint4 *>(otile + ((r * T + s) * ECD_CHUNK) +
+                                                             ((((q >> 2) ^ (s & 3u)) << 6) |
+                                                              ((q & 3u) << 4)));
+            if (ost < a.nstripes) {
+                uint8_t *g = a.out_base[r] + ost * a.out_stride + q * 16u;
+                if constexpr (NTS) {
+                    const v4u w = {v.x, v.y, v.z, v.w};
+                    __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(g));
+                } else {
+                    *reinterpret_cast<uint4 *>(g) = v;
+                }
+            }
+        }
+    }
+}
+
+template <int TS>
+inline uint64_t combine_grid(uint64_t nstripes)
+{
+    return (nstripes + 8 * TS - 1) / (8 * TS);
+}
+
+template <int TS, bool OST>
+inline size_t combine_lds(u32 k, u32 rows)
+{
+    return (size_t)(k + (OST ? rows : 0)) * 8 * TS * ECD_CHUNK;
+}
+
+} // namespace ecdev
+
+#endif

@@ -1,0 +1,73 @@
+"""Stripe-range sharding across processes (one process per MI355X).
+
+Stripes are independent, so an N-GPU job is a contiguous
+stripe-range partition with no data-path collective.  The only collectives
+here are control plane: a barrier around timed regions, the max over ranks of
+the elapsed time, and an all-ranks-ok flag.  Backend: "nccl" (RCCL) when the
+ranks own GPUs, "gloo" otherwise (CPU tests).
+"""
+import os
+
+
+def env_rank():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def stripe_range(rank, world, nstripes, align=1):
+    """Contiguous [s0, s1) of rank `rank`; boundaries are multiples of
+    `align` (pattern groups) except the final end."""
+    units = (nstripes + align - 1) // align
+    s0 = min(nstripes, units * rank // world * align)
+    s1 = min(nstripes, units * (rank + 1) // world * align)
+    return s0, s1
+
+
+class Group:
+    """torch.distributed wrapper that degrades to no-ops for world == 1."""
+
+    def __init__(self, backend=None):
+        self.rank, self.world, self.local = env_rank()
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            if backend is None:
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if not dist.is_initialized():
+                dist.init_process_group(backend=backend)
+            self.dist = dist
+            self.backend = backend
+        else:
+            self.backend = None
+
+    def _dev(self):
+        import torch
+        if self.backend == "nccl":
+            return torch.device("cuda", self.local)
+        return torch.device("cpu")
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return float(x)
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self._dev())
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_ok(self, ok):
+        if not self.dist:
+            return bool(ok)
+        import torch
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self._dev())
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def close(self):
+        if self.dist and self.dist.is_initialized():
+            self.dist.barrier()
+            self.dist.destroy_process_group()

@@ -1,0 +1,121 @@
+"""The C-ABI boundary on CPU: the library loads, exports every symbol
+include/ec_method.h declares, keeps the 120-byte ec_matrix_list_t layout, and
+its host-side math (GF(2^8), encode matrix, inverse) matches the oracle.  No
+compute call is made without a GPU: ec_method_init must fail with -ENODEV."""
+import ctypes
+import itertools
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "ec_method.h")
+LIB = os.path.join(ROOT, "glusterfs_amd", "lib", "libec_mi355x.so")
+
+
+def declared():
+    text = open(HDR).read()
+    return sorted(set(re.findall(r"\b(ec_method_\w+)\s*\(", text)))
+
+
+def test_header_matches_python_mirror():
+    import glusterfs_amd.ec_method as m
+    assert sorted(m.EXPORTS) == declared()
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True,
+                         text=True, check=True).stdout
+    syms = set(l.split()[-1] for l in out.splitlines() if " T " in l)
+    missing = [s for s in declared() if s not in syms]
+    assert not missing, missing
+    lib = ctypes.CDLL(LIB)
+    for s in declared():
+        assert getattr(lib, s)
+
+
+def test_reference_prototypes_unchanged():
+    """The five drop-in prototypes are those of ec-method.h:31-46."""
+    text = " ".join(open(HDR).read().split())
+    for proto in (
+        "int32_t ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, "
+        "uint32_t rows, uint32_t max, const char *gen);",
+        "void ec_method_fini(ec_matrix_list_t *list);",
+        "int32_t ec_method_update(xlator_t *xl, ec_matrix_list_t *list, const char *gen);",
+        "void ec_method_encode(ec_matrix_list_t *list, uint64_t size, void *in, void **out);",
+        "int32_t ec_method_decode(ec_matrix_list_t *list, uint64_t size, uintptr_t mask, "
+        "uint32_t *rows, void **in, void *out);",
+    ):
+        assert proto in text, proto
+
+
+def _build_c_check(tmp_path):
+    exe = str(tmp_path / "abi_check")
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", "abi_check.c"), "-o", exe,
+                    "-L", os.path.dirname(LIB), "-lec_mi355x",
+                    "-Wl,-rpath," + os.path.dirname(LIB)], check=True)
+    return exe
+
+
+def test_c_caller_layout_and_no_gpu_failure(tmp_path):
+    import glusterfs_amd
+    if glusterfs_amd.device_count() > 0:
+        pytest.skip("a GPU is visible: covered by tests/test_gpu_parity.py")
+    exe = _build_c_check(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "init=-19" in r.stdout            # -ENODEV: fails loudly, no CPU path
+
+
+@pytest.mark.gpu
+def test_c_caller_roundtrip_on_gpu(tmp_path):
+    exe = _build_c_check(tmp_path)
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "roundtrip ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_python_init_fails_without_gpu():
+    import glusterfs_amd as g
+    if g.device_count() > 0:
+        pytest.skip("GPU visible")
+    with pytest.raises(OSError) as e:
+        g.ECMatrixList(4, 6)
+    assert e.value.errno == 19
+
+
+def test_host_matrices_match_oracle(oracle):
+    import glusterfs_amd as g
+    for k, n in ((2, 3), (4, 6), (8, 12), (16, 20), (16, 31), (5, 7)):
+        assert np.array_equal(np.array(g.encode_matrix(k, n)), oracle.encode_matrix(k, n))
+    rng = np.random.default_rng(3)
+    for k, n in ((2, 3), (3, 5), (4, 6), (8, 12), (16, 20), (16, 31)):
+        if n <= 12:
+            picks = list(itertools.combinations(range(1, n + 1), k))
+        else:
+            picks = [sorted(rng.choice(n, k, replace=False) + 1) for _ in range(60)]
+        for rows in picks:
+            rows = [int(r) for r in rows]
+            assert g.inverse_matrix(list(rows)) == oracle.inverse_matrix(list(rows)).tolist()
+
+
+def test_host_gf_semantics():
+    import glusterfs_amd as g
+    from test_oracle import py_gf_mul, py_gf_inv
+    for a in range(256):
+        for b in (0, 1, 7, 0x80, 0xFF):
+            assert g.gf_mul(a, b) == py_gf_mul(a, b)
+    for a in range(1, 256):
+        assert g.gf_div(1, a) == py_gf_inv(a)
+    assert g.gf_mul(300, 1) == 256 and g.gf_div(5, 0) == 256
+
+
+def test_inverse_rejects_bad_rows():
+    import glusterfs_amd as g
+    with pytest.raises(OSError):
+        g.inverse_matrix([1, 1, 2, 3])       # repeated evaluation point
+    with pytest.raises(OSError):
+        g.inverse_matrix([0, 1, 2, 3])       # rows are brick index + 1 >= 1

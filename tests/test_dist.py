@@ -1,0 +1,84 @@
+"""N>1 path on CPU: two gloo ranks shard a disperse job by stripe range
+(glusterfs_amd/dist.py, the code bench.py runs under torch.distributed.run)
+and the union of their shards equals the single-process result.  The per-rank
+compute is the CPU oracle (test stand-in for the GPU kernel)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, k, n, nstripes, group, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle")]
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import oracle as O
+    from glusterfs_amd.dist import Group, stripe_range
+
+    g = Group(backend="gloo")
+    data = O.fill_xorshift(512 * k * nstripes)
+    s0, s1 = stripe_range(g.rank, g.world, nstripes, align=group)
+    mine = O.encode(k, n, data[s0 * 512 * k:s1 * 512 * k]) if s1 > s0 else \
+        [np.zeros(0, np.uint8)] * n
+    # gather shards (test-only collective) and compare with the full encode
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    g.dist.all_gather(sizes, torch.tensor([s1 - s0]))
+    full = O.encode(k, n, data)
+    ok = True
+    for i in range(n):
+        buf = torch.zeros(max(int(x.item()) for x in sizes) * 512, dtype=torch.uint8)
+        buf[:(s1 - s0) * 512] = torch.from_numpy(mine[i])
+        parts = [torch.zeros_like(buf) for _ in range(world)]
+        g.dist.all_gather(parts, buf)
+        cat = np.concatenate([p[:int(sz.item()) * 512].numpy() for p, sz in zip(parts, sizes)])
+        ok &= np.array_equal(cat, full[i])
+    elapsed = g.max(0.5 + rank)          # max-over-ranks timing
+    ok = g.all_ok(ok)
+    g.close()
+    q.put((rank, ok, elapsed, s0, s1))
+
+
+@pytest.mark.parametrize("nstripes,group", [(1000, 1), (999, 16), (7, 1)])
+def test_two_rank_stripe_partition(nstripes, group):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    ps = [ctx.Process(target=_worker, args=(r, world, port, 4, 6, nstripes, group, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] for r in res)
+    assert all(r[2] == 1.5 for r in res)           # max over ranks of 0.5 + rank
+    assert res[0][3] == 0 and res[-1][4] == nstripes
+    assert res[0][4] == res[1][3]                   # contiguous, disjoint
+    if group > 1:
+        assert res[0][4] % group == 0
+
+
+def test_stripe_range_properties():
+    from glusterfs_amd.dist import stripe_range
+    for n in (0, 1, 7, 1000, 524288):
+        for w in (1, 2, 3, 8):
+            for al in (1, 8, 1024):
+                rs = [stripe_range(r, w, n, al) for r in range(w)]
+                assert rs[0][0] == 0 and rs[-1][1] == n
+                for (a0, a1), (b0, b1) in zip(rs, rs[1:]):
+                    assert a1 == b0 and a0 <= a1
+                    assert a1 % al == 0 or a1 == n

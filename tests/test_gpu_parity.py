@@ -156,16 +156,16 @@ def test_encode_advances_out_pointers(ec, oracle):
         assert np.array_equal(bufs[i], want[i])
 
 
-@pytest.mark.parametrize("k,n", [(4, 6), (8, 12)])
-def test_decode_mixed_patterns(ec, oracle, k, n):
-    group = 16
+@pytest.mark.parametrize("k,n,group", [(4, 6, 8), (4, 6, 16), (8, 12, 16), (8, 12, 64),
+                                       (16, 20, 8), (3, 5, 32)])
+def test_decode_mixed_patterns(ec, oracle, k, n, group):
     ngroups = 23
     nstripes = group * ngroups - 5          # ragged last group
     data = rand_bytes(CHUNK * k * nstripes, seed=21)
     frags = oracle.encode(k, n, data)
-    combos = list(itertools.combinations(range(n), k))
     rng = np.random.default_rng(4)
-    masks = [sum(1 << b for b in combos[i]) for i in rng.choice(len(combos), ngroups)]
+    pool = [sum(1 << int(b) for b in rng.choice(n, k, replace=False)) for _ in range(5)]
+    masks = [pool[i] for i in rng.integers(0, len(pool), ngroups)]
     out = np.zeros(CHUNK * k * nstripes, np.uint8)
     with ec.ECMatrixList(k, n) as L:
         L.decode_mixed(nstripes, group, masks, frags, out)
@@ -216,3 +216,29 @@ def test_concurrent_callers(ec, oracle):
         for t in th:
             t.join()
     assert not errors
+
+
+def test_mixed_and_heal_device(ec, oracle, torch_cuda):
+    torch = torch_cuda
+    k, n, nst, group = 8, 12, 4096, 512
+    data = rand_bytes(CHUNK * k * nst, seed=41)
+    frags = oracle.encode(k, n, data)
+    dfr = [torch.from_numpy(f).cuda() for f in frags]
+    masks = [0xFF0, 0xEB5 | 0x0, 0x0FF, 0xF0F]
+    masks = [m for m in masks if bin(m).count("1") == k]
+    gp = torch.tensor([i % len(masks) for i in range(nst // group)], dtype=torch.uint8,
+                      device="cuda")
+    out = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed_device(0, None, nst, group, gp, masks, dfr, out)
+        ec.sync_device(0)
+        assert np.array_equal(out.cpu().numpy(), data)
+        mask = 0xEB5
+        good = [b for b in range(n) if (mask >> b) & 1]
+        target = ((1 << n) - 1) & ~mask
+        tgt = [b for b in range(n) if (target >> b) & 1]
+        outs = [torch.empty(CHUNK * nst, dtype=torch.uint8, device="cuda") for _ in tgt]
+        L.heal_device(0, None, nst, mask, [dfr[b] for b in good], target, outs)
+        ec.sync_device(0)
+        for o, b in zip(outs, tgt):
+            assert np.array_equal(o.cpu().numpy(), frags[b])

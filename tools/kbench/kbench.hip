@@ -1,0 +1,319 @@
+/*
+ * kbench.hip -- development harness (not product): A/B the shipped kernel
+ * templates of glusterfs_amd/csrc/ec_kernels_impl.h over their tuning knobs,
+ * next to HBM calibration kernels, in ONE process with interleaved rounds and
+ * the median of rounds (cdna_hip_programming.md 5.4 rule 24).  Each variant's
+ * output is compared with the group's first variant.
+ *
+ *   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I glusterfs_amd/csrc \
+ *         tools/kbench/kbench.hip -o tools/kbench/kbench
+ *   tools/kbench/kbench [GiB=1] [rounds=7]
+ */
+#include "../../glusterfs_amd/csrc/ec_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CHK(x)                                                                             \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);  \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+/* ---------------------------------------------------------- calibration */
+__global__ void k_copy(const uint4 *__restrict__ a, uint4 *__restrict__ b, size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        b[i] = a[i];
+}
+
+__global__ void k_copy_nt(const uint4 *__restrict__ a, uint4 *__restrict__ b, size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(a + i));
+        __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(b + i));
+    }
+}
+
+__global__ void k_read(const uint4 *__restrict__ a, size_t n, u32 *sink)
+{
+    u32 x = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 v = a[i];
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (x == 0x12345678u)
+        sink[0] = x;
+}
+
+__global__ void k_write(uint4 *__restrict__ b, size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        b[i] = make_uint4((u32)i, (u32)i, (u32)i, (u32)i);
+}
+
+/* our access shape: 8 lanes x 8 B cover one 64-B plane segment, a wave
+ * instruction covers 8 stripes' segments at a 512-B stride */
+__global__ void k_write_seg(uint8_t *__restrict__ b, size_t nchunks)
+{
+    const size_t gt = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t ch = gt / 8;
+    if (ch >= nchunks)
+        return;
+    const u32 c = (gt % 8) * 8;
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+        *reinterpret_cast<uint2 *>(b + ch * 512 + p * 64 + c) = make_uint2((u32)gt, p);
+}
+
+__global__ void k_read_seg(const uint8_t *__restrict__ a, size_t nchunks, u32 *sink)
+{
+    const size_t gt = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t ch = gt / 8;
+    if (ch >= nchunks)
+        return;
+    const u32 c = (gt % 8) * 8;
+    u32 x = 0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(a + ch * 512 + p * 64 + c);
+        x ^= v.x ^ v.y;
+    }
+    if (x == 0x12345678u)
+        sink[0] = x;
+}
+
+struct Variant {
+    std::string name;
+    double bytes;                  /* algorithmic bytes per launch */
+    std::function<void(hipStream_t)> fn;
+    uint8_t *out;                  /* checked region (nullptr: no check) */
+    size_t out_bytes;
+};
+
+static void fill(uint8_t *d, size_t n, uint32_t seed)
+{
+    std::vector<uint32_t> h(n / 4);
+    uint32_t x = seed | 1;
+    for (auto &w : h) {
+        x ^= x << 13;
+        x ^= x >> 17;
+        x ^= x << 5;
+        w = x;
+    }
+    CHK(hipMemcpy(d, h.data(), n, hipMemcpyHostToDevice));
+}
+
+static void run_group(const char *title, std::vector<Variant> &vars, int rounds, int iters,
+                      hipStream_t s)
+{
+    std::vector<uint8_t> ref, cur;
+    for (size_t v = 0; v < vars.size(); ++v) {
+        if (!vars[v].out)
+            continue;
+        CHK(hipMemset(vars[v].out, 0, vars[v].out_bytes));
+        vars[v].fn(s);
+        CHK(hipStreamSynchronize(s));
+        cur.resize(vars[v].out_bytes);
+        CHK(hipMemcpy(cur.data(), vars[v].out, vars[v].out_bytes, hipMemcpyDeviceToHost));
+        if (ref.empty())
+            ref = cur;
+        else if (cur != ref)
+            printf("  MISMATCH %s\n", vars[v].name.c_str());
+    }
+    hipEvent_t e0, e1;
+    CHK(hipEventCreate(&e0));
+    CHK(hipEventCreate(&e1));
+    std::vector<std::vector<double>> t(vars.size());
+    for (int rd = 0; rd < rounds; ++rd)
+        for (size_t v = 0; v < vars.size(); ++v) {
+            vars[v].fn(s);
+            vars[v].fn(s);
+            CHK(hipEventRecord(e0, s));
+            for (int i = 0; i < iters; ++i)
+                vars[v].fn(s);
+            CHK(hipEventRecord(e1, s));
+            CHK(hipEventSynchronize(e1));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            t[v].push_back(ms / iters);
+        }
+    printf("== %s\n%-34s %9s %9s %9s %7s\n", title, "variant", "ms(med)", "ms(min)", "GB/s",
+           "frac8T");
+    for (size_t v = 0; v < vars.size(); ++v) {
+        std::sort(t[v].begin(), t[v].end());
+        const double med = t[v][t[v].size() / 2];
+        printf("%-34s %9.4f %9.4f %9.1f %7.3f\n", vars[v].name.c_str(), med, t[v][0],
+               vars[v].bytes / med / 1e6, vars[v].bytes / med / 1e6 / 8000.0);
+    }
+    fflush(stdout);
+}
+
+/* decode k+r with the first r bricks missing, coefficients from the host
+ * inverse (a dense k x k matrix is all we need for timing; correctness of
+ * the math is covered by the parity tests -- here variants are compared
+ * with each other). */
+template <int K>
+static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const *frags,
+                       uint8_t *out, const uint8_t *coef)
+{
+    ecd_combine_desc_t d;
+    memset(&d, 0, sizeof(d));
+    d.k = K;
+    d.rows = K;
+    d.nstripes = nst;
+    d.in_stride = ECD_CHUNK;
+    d.out_stride = (uint64_t)K * ECD_CHUNK;
+    for (int p = 0; p < K; ++p) {
+        d.in_base[p] = frags[p];
+        d.pat[p] = (uint8_t)p;
+    }
+    for (int r = 0; r < K; ++r)
+        d.out_base[r] = out + (uint64_t)r * ECD_CHUNK;
+    memcpy(d.pat + K, coef, K * K);
+    d.npatterns = 1;
+    d.pat_bytes = K + K * K;
+    static CombineArgs a;
+    if (ecdk_pack_args(&d, &a))
+        exit(2);
+    const double bytes = 2.0 * nst * K * ECD_CHUNK;
+    const size_t ob = (size_t)nst * K * ECD_CHUNK;
+    auto add = [&](const char *nm, auto kern, int ts, bool ost) {
+        const size_t lds = (size_t)K * (ost ? 2 : 1) * 8 * ts * ECD_CHUNK;
+        const uint64_t g = (nst + 8 * ts - 1) / (8 * ts);
+        vars.push_back({nm, bytes, [=](hipStream_t s) {
+                            hipLaunchKernelGGL(kern, dim3((u32)g), dim3(kBlock), lds, s, a);
+                        }, out, ob});
+    };
+    add("combine TS1", ec_combine<K, 1, false, false, false>, 1, false);
+    add("combine TS2", ec_combine<K, 2, false, false, false>, 2, false);
+    add("combine TS1 OST", ec_combine<K, 1, false, false, true>, 1, true);
+    add("combine TS2 OST", ec_combine<K, 2, false, false, true>, 2, true);
+    add("combine TS1 OST NTS", ec_combine<K, 1, false, true, true>, 1, true);
+}
+
+template <int K, int N, typename KF>
+static void add_encode_w(std::vector<Variant> &vars, const char *nm, uint64_t nst,
+                         const uint8_t *in, const FragPtrs &f, KF kern, int W)
+{
+    const double bytes = (double)nst * (K + N) * ECD_CHUNK;
+    const uint64_t g = (nst * (16 / W) + kBlock - 1) / kBlock;
+    vars.push_back({nm, bytes, [=](hipStream_t s) {
+                        hipLaunchKernelGGL(kern, dim3((u32)g), dim3(kBlock), 0, s, in, f, nst);
+                    }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+}
+
+int main(int argc, char **argv)
+{
+    const double gib = argc > 1 ? atof(argv[1]) : 1.0;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 7;
+    const int iters = 10;
+    hipDeviceProp_t prop;
+    CHK(hipGetDeviceProperties(&prop, 0));
+    printf("device %s CUs %d, %.2f GiB user data per launch\n", prop.gcnArchName,
+           prop.multiProcessorCount, gib);
+    hipStream_t s;
+    CHK(hipStreamCreate(&s));
+    const uint64_t user = (uint64_t)(gib * (1ull << 30));
+    uint8_t *bufA, *bufB;
+    CHK(hipMalloc(&bufA, user * 3));   /* inputs / fragments */
+    CHK(hipMalloc(&bufB, user * 3));   /* outputs */
+    fill(bufA, user * 3, 12345);
+
+    {   /* calibration */
+        std::vector<Variant> v;
+        const size_t n16 = user / 16;
+        const int grid = prop.multiProcessorCount * 8;
+        u32 *sink = reinterpret_cast<u32 *>(bufB + user * 3 - 64);
+        v.push_back({"copy uint4", 2.0 * user, [=](hipStream_t st) {
+                         hipLaunchKernelGGL(k_copy, dim3(grid), dim3(256), 0, st,
+                                            (const uint4 *)bufA, (uint4 *)bufB, n16);
+                     }, nullptr, 0});
+        v.push_back({"copy uint4 NT", 2.0 * user, [=](hipStream_t st) {
+                         hipLaunchKernelGGL(k_copy_nt, dim3(grid), dim3(256), 0, st,
+                                            (const uint4 *)bufA, (uint4 *)bufB, n16);
+                     }, nullptr, 0});
+        v.push_back({"read-only", 1.0 * user, [=](hipStream_t st) {
+                         hipLaunchKernelGGL(k_read, dim3(grid), dim3(256), 0, st,
+                                            (const uint4 *)bufA, n16, sink);
+                     }, nullptr, 0});
+        v.push_back({"write-only", 1.0 * user, [=](hipStream_t st) {
+                         hipLaunchKernelGGL(k_write, dim3(grid), dim3(256), 0, st, (uint4 *)bufB,
+                                            n16);
+                     }, nullptr, 0});
+        const size_t nch = user / 512;
+        const u32 sg = (u32)((nch * 8 + 255) / 256);
+        v.push_back({"read-only 64B segs", 1.0 * user, [=](hipStream_t st) {
+                         hipLaunchKernelGGL(k_read_seg, dim3(sg), dim3(256), 0, st,
+                                            (const uint8_t *)bufA, nch, sink);
+                     }, nullptr, 0});
+        v.push_back({"write-only 64B segs", 1.0 * user, [=](hipStream_t st) {
+                         hipLaunchKernelGGL(k_write_seg, dim3(sg), dim3(256), 0, st, bufB, nch);
+                     }, nullptr, 0});
+        run_group("HBM calibration", v, rounds, iters, s);
+    }
+    {   /* 4+2 decode */
+        const uint64_t nst = user / (4 * ECD_CHUNK);
+        uint8_t *fr[4];
+        for (int p = 0; p < 4; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        const uint8_t inv[16] = {0xcb, 0x5d, 0xdd, 0x4b, 0x4b, 0x00, 0xdd, 0x96,
+                                 0xa7, 0x8c, 0x03, 0x28, 0xd2, 0xd5, 0x04, 0x02};
+        std::vector<Variant> v;
+        add_decode<4>(v, nst, fr, bufB, inv);
+        run_group("decode 4+2 mask 0x3C", v, rounds, iters, s);
+    }
+    {   /* 8+4 decode: a dense pseudo-random nonzero matrix */
+        const uint64_t nst = user / (8 * ECD_CHUNK);
+        uint8_t *fr[8];
+        for (int p = 0; p < 8; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        uint8_t c[64];
+        for (int i = 0; i < 64; ++i)
+            c[i] = (uint8_t)(1 + (i * 97 + 31) % 255);
+        std::vector<Variant> v;
+        add_decode<8>(v, nst, fr, bufB, c);
+        run_group("decode 8+4 dense", v, rounds, iters, s);
+    }
+    {   /* encode 4+2, 8+4, 16+4 */
+        auto frag_ptrs = [&](uint64_t nst, int n) {
+            FragPtrs f;
+            for (int i = 0; i < n; ++i)
+                f.p[i] = bufB + (uint64_t)i * nst * ECD_CHUNK;
+            return f;
+        };
+        std::vector<Variant> v;
+        uint64_t nst = user / (4 * ECD_CHUNK);
+        FragPtrs f = frag_ptrs(nst, 6);
+        add_encode_w<4, 6>(v, "enc 4+2 W1", nst, bufA, f, ec_encode_vander<4, 6, 1, false>, 1);
+        add_encode_w<4, 6>(v, "enc 4+2 W2", nst, bufA, f, ec_encode_vander<4, 6, 2, false>, 2);
+        add_encode_w<4, 6>(v, "enc 4+2 W4", nst, bufA, f, ec_encode_vander<4, 6, 4, false>, 4);
+        add_encode_w<4, 6>(v, "enc 4+2 W2 NTS", nst, bufA, f, ec_encode_vander<4, 6, 2, true>, 2);
+        run_group("encode 4+2", v, rounds, iters, s);
+        v.clear();
+        nst = user / (8 * ECD_CHUNK);
+        f = frag_ptrs(nst, 12);
+        add_encode_w<8, 12>(v, "enc 8+4 W1", nst, bufA, f, ec_encode_vander<8, 12, 1, false>, 1);
+        add_encode_w<8, 12>(v, "enc 8+4 W2", nst, bufA, f, ec_encode_vander<8, 12, 2, false>, 2);
+        add_encode_w<8, 12>(v, "enc 8+4 W1 NTS", nst, bufA, f, ec_encode_vander<8, 12, 1, true>, 1);
+        run_group("encode 8+4", v, rounds, iters, s);
+        v.clear();
+        nst = user / (16 * ECD_CHUNK);
+        f = frag_ptrs(nst, 20);
+        add_encode_w<16, 20>(v, "enc 16+4 W1", nst, bufA, f, ec_encode_vander<16, 20, 1, false>, 1);
+        add_encode_w<16, 20>(v, "enc 16+4 W1 NTS", nst, bufA, f, ec_encode_vander<16, 20, 1, true>, 1);
+        run_group("encode 16+4", v, rounds, iters, s);
+    }
+    return 0;
+}

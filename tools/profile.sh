@@ -1,0 +1,26 @@
+#!/bin/bash
+# rocprofv3 profiles of the dominant kernels (run on the GPU box via gpurun).
+# Pass 1: --kernel-trace --stats; passes 2/3: PMC FETCH_SIZE and WRITE_SIZE
+# (separate passes: they do not fit one TCC slot set, MI355X_MICROARCH.md).
+# Usage: tools/profile.sh TAG CONFIG GIB [CONFIG GIB ...]
+#   CONFIG = dec:4+2:3C | enc:4+2 | enc:8+4 | dec:8+4:FF0 ...
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; shift
+cd /tmp && export TMPDIR=/tmp
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+while [ $# -ge 2 ]; do
+  CFG=$1; GIB=$2; shift 2
+  NAME=$(echo "$CFG" | tr ':+' '_p')
+  for PASS in trace FETCH_SIZE WRITE_SIZE; do
+    if [ $PASS = trace ]; then ARGS="--kernel-trace --stats"; else ARGS="--kernel-trace --pmc $PASS"; fi
+    echo "[$(date +%T)] $CFG $PASS"
+    timeout -k 10 300 rocprofv3 $ARGS -d "$OUT/${NAME}_$PASS" -o run --output-format csv -- \
+      python3 "$R/bench.py" --only "$CFG" --gib "$GIB" --steps 10 --warmup 2 \
+      > "$OUT/${NAME}_$PASS.log" 2>&1
+    rc=$?
+    echo "rc=$rc"; tail -2 "$OUT/${NAME}_$PASS.log"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+  done
+done
