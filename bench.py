@@ -296,11 +296,12 @@ def main():
     args = parse()
     import torch
     import glusterfs_amd as g
-    from glusterfs_amd.dist import Group
+    from glusterfs_amd.dist import Group, local_device_index
 
+    dev_index = local_device_index()
+    torch.cuda.set_device(dev_index)          # before the process group (NCCL)
     grp = Group()
-    torch.cuda.set_device(grp.local)
-    dev = torch.device("cuda", grp.local)
+    dev = torch.device("cuda", dev_index)
     c = Ctx(g, torch, dev)
     nbytes = int(args.gib * (1 << 30))
     if args.only:

@@ -14,6 +14,13 @@ def env_rank():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def local_device_index():
+    """GPU of this rank: LOCAL_RANK, unless EC_BENCH_DEVICE pins every rank
+    to one device (multi-rank rehearsal on a one-GPU box, with gloo)."""
+    forced = os.environ.get("EC_BENCH_DEVICE")
+    return int(forced) if forced is not None else env_rank()[2]
+
+
 def stripe_range(rank, world, nstripes, align=1):
     """Contiguous [s0, s1) of rank `rank`; boundaries are multiples of
     `align` (pattern groups) except the final end."""
@@ -33,7 +40,8 @@ class Group:
             import torch
             import torch.distributed as dist
             if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
+                backend = os.environ.get("EC_BENCH_BACKEND") or (
+                    "nccl" if torch.cuda.is_available() else "gloo")
             if not dist.is_initialized():
                 dist.init_process_group(backend=backend)
             self.dist = dist
@@ -44,12 +52,15 @@ class Group:
     def _dev(self):
         import torch
         if self.backend == "nccl":
-            return torch.device("cuda", self.local)
+            return torch.device("cuda", local_device_index())
         return torch.device("cpu")
 
     def barrier(self):
         if self.dist:
-            self.dist.barrier()
+            if self.backend == "nccl":
+                self.dist.barrier(device_ids=[local_device_index()])
+            else:
+                self.dist.barrier()
 
     def max(self, x):
         if not self.dist:
@@ -69,5 +80,5 @@ class Group:
 
     def close(self):
         if self.dist and self.dist.is_initialized():
-            self.dist.barrier()
+            self.barrier()
             self.dist.destroy_process_group()

@@ -52,14 +52,18 @@ def algorithmic(cfg, gib):
     kind, geo = cfg.split("_")[0], cfg.split("_")[1]
     k, r = map(int, geo.split("p"))
     S = int(gib * (1 << 30)) // (512 * k) * 512 * k
-    return S, (S * (k + k + r) // k if kind == "enc" else 2 * S)
+    if kind == "enc":
+        return S, S * (k + k + r) // k
+    if kind == "heal":
+        return S, S + S * r // k
+    return S, 2 * S
 
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     traffic_path = sys.argv[3] if len(sys.argv) > 3 else None
     gib = {"dec_4p2_3C": 1, "enc_4p2": 1, "enc_8p4": 0.25, "dec_8p4_FF0": 0.25,
-           "enc_16p4": 2, "dec_8p4_EB5": 0.25, "dec_4p2_0F": 1}
+           "enc_16p4": 2, "dec_8p4_EB5": 0.25, "dec_4p2_0F": 1, "mixed_8p4": 1, "heal_8p4": 1}
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     lines = ["# rocprofv3 summary (%s)" % os.path.basename(src.rstrip("/")), "",
              "| config | kernel | calls | avg us | user GB/s | algorithmic GB/s | HBM frac "
@@ -77,6 +81,10 @@ def main():
         # encode configs also run one decode for the parity check
         if cfg.startswith("enc"):
             kern = next((k for k in st if "encode" in k), kern)
+        elif any(k.startswith("ec_combine") for k in st):
+            # the timed combine launches dominate the one setup encode
+            kern = max((k for k in st if k.startswith("ec_combine")),
+                       key=lambda k: st[k]["calls"])
         s = st[kern]
         rd = fs.get(kern, 0) * 1024 * 2
         wr = ws.get(kern, 0) * 1024
