@@ -7,10 +7,12 @@
  *            W = 4 / 2 / 1 / 1 dwords per plane per lane (VGPR budget);
  *            non-temporal stores for 16+4 only (+2.5 %; neutral or worse
  *            elsewhere)
- *   combine  one tile per 256-thread block: 16 stripes for k <= 4 (+3-4 %),
- *            8 stripes above (LDS per block caps occupancy); outputs stored
- *            straight from registers (staging them through LDS measured
- *            equal at k = 4 and -36 % at k = 8)
+ *   combine  one tile per block, staged by LDS-DMA (global_load_lds_dwordx4):
+ *            k <= 4: 16-stripe tiles, 4 waves; k > 4: 8-stripe tiles (LDS per
+ *            block caps occupancy), 8 waves -- measured (profiles/kbench_r01_*)
+ *            8+4 decode 0.57 -> 0.66, 16+4 decode 0.24 -> 0.42, mixed 8+4
+ *            0.55 -> 0.63 of 8 TB/s against 4-wave register staging; outputs
+ *            are stored straight from registers
  */
 #include <hip/hip_runtime.h>
 
@@ -41,7 +43,7 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-template <int K, int TS>
+template <int K, int TS, int NW>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     const uint64_t g = combine_grid<TS>(a.nstripes);
@@ -49,13 +51,13 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    const size_t lds = combine_lds<TS, false>(a.k, a.rows);
+    const size_t lds = combine_lds<TS>(a.k);
     if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, true, false, false>), dim3((u32)g), dim3(kBlock),
-                           lds, s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, true, false, true>), dim3((u32)g),
+                           dim3(NW * 64), lds, s, a);
     else
-        hipLaunchKernelGGL((ec_combine<K, TS, false, false, false>), dim3((u32)g), dim3(kBlock),
-                           lds, s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, false, true>), dim3((u32)g),
+                           dim3(NW * 64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -124,10 +126,10 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
         return rc;
     /* a 16-stripe tile must not straddle two pattern groups */
     if (d->k <= 4 && (!d->group_pattern || d->group_shift >= 4))
-        return launch_combine<4, 2>(s, a);
+        return launch_combine<4, 2, 4>(s, a);
     if (d->k <= 4)
-        return launch_combine<4, 1>(s, a);
+        return launch_combine<4, 1, 4>(s, a);
     if (d->k <= 8)
-        return launch_combine<8, 1>(s, a);
-    return launch_combine<16, 1>(s, a);
+        return launch_combine<8, 1, 8>(s, a);
+    return launch_combine<16, 1, 8>(s, a);
 }

@@ -31,8 +31,10 @@
  *
  * Tuning knobs measured with tools/kbench (profiles/kbench_*.log): one tile
  * per block beats a persistent grid with register prefetch (vmcnt also counts
- * the stores of the previous tile, which serialises the prefetch), and
- * non-temporal loads lose; NTS (non-temporal stores) is kept as a knob.
+ * the stores of the previous tile, which serialises the prefetch);
+ * non-temporal loads lose; staging the output tile through LDS and a split
+ * 16+16-case dispatch measured equal or worse and were removed; NTS
+ * (non-temporal stores) and the block size NW remain knobs.
  */
 #ifndef EC_MI355X_KERNELS_IMPL_H
 #define EC_MI355X_KERNELS_IMPL_H
@@ -52,6 +54,16 @@ typedef u32 v2u __attribute__((ext_vector_type(2)));
 typedef u32 v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
+
+/* Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E). */
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 
 template <int W>
 __device__ __forceinline__ void load_plane(const uint8_t *p, u32 (&d)[W])
@@ -220,108 +232,131 @@ __device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
     return __builtin_amdgcn_readfirstlane((w >> ((idx & 3u) * 8u)) & 0xFFu);
 }
 
-template <int K, int TS, bool MIXED, bool NTS, bool OST>
-__global__ __launch_bounds__(kBlock) void ec_combine(const CombineArgs a)
+/* K: max inputs (k <= K); TS: tile = 8*TS stripes; NW: waves per block;
+ * GLDS: stage the tile with LDS-DMA (global_load_lds_dwordx4, no VGPRs)
+ * instead of global_load + ds_write; PF: issue the next input's LDS reads
+ * before each multiply. */
+template <int K, int TS, int NW, bool MIXED, bool NTS, bool GLDS = false, bool PF = false>
+__global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
-    constexpr u32 T = 8 * TS; /* stripes per tile */
-    constexpr int CW = 2;     /* dwords per plane per lane in the compute */
+    constexpr u32 T = 8 * TS;            /* stripes per tile                   */
+    constexpr u32 NT = NW * 64;          /* threads per block                  */
+    constexpr u32 PER = (K * T * 32 + NT - 1) / NT; /* staged pieces per thread */
+    constexpr int CW = 2;                /* dwords per plane per lane (compute) */
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
     const u32 k = a.k;
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
-    uint8_t *const otile = lds + (size_t)k * T * ECD_CHUNK; /* OST: output tile */
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
 
     u32 pb = 0;
     if constexpr (MIXED)
         pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
 
-    /* stage: 256 threads load 16-byte pieces (32 per chunk), coalesced */
-    {
-        const u32 ls = tid >> 5, lq = tid & 31u;
-        uint4 v[K][TS];
+    if constexpr (GLDS) {
+        /* every wave instruction fills 1 KiB of LDS linearly (2 chunks of one
+         * input); the XOR plane rotation is applied to the per-lane source
+         * address instead of the destination */
+        constexpr u32 NI = K * T * 32 / 64; /* wave instructions per tile */
 #pragma unroll
-        for (int p = 0; p < K; ++p) {
-            const u32 src = (u32)p < k ? pat_byte(a, pb, (u32)p) : 0u;
+        for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
+            const u32 ins = j * NW + wave;           /* wave-uniform */
+            if (ins >= NI)
+                break;
+            const u32 p = ins / (T / 2);
+            if (p >= k)
+                break;
+            const u32 e = ins * 64 + lane;            /* LDS piece */
+            const u32 s = (e / 32) % T, slot = e & 31u;
+            const uint64_t st = t0 + s;
+            if (st < a.nstripes) {
+                const u32 src = pat_byte(a, pb, p);
+                const uint8_t *g = a.in_base[src] + st * a.in_stride +
+                                   ((((slot >> 2) ^ (s & 3u)) << 6) | ((slot & 3u) << 4));
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)g,
+                    (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+            }
+        }
+    } else {
+        /* stage: 16-byte pieces e = (input p, stripe s, piece q), coalesced */
+        uint4 v[PER];
 #pragma unroll
-            for (int j = 0; j < TS; ++j) {
-                const uint64_t st = t0 + ls + 8u * j;
-                v[p][j] = make_uint4(0, 0, 0, 0);
-                if ((u32)p < k && st < a.nstripes)
-                    v[p][j] = *reinterpret_cast<const uint4 *>(a.in_base[src] +
-                                                               st * a.in_stride + lq * 16u);
+        for (u32 j = 0; j < PER; ++j) {
+            const u32 e = tid + j * NT;
+            const u32 p = e / (T * 32), s = (e / 32) % T, q = e & 31u;
+            const uint64_t st = t0 + s;
+            v[j] = make_uint4(0, 0, 0, 0);
+            if (p < k && st < a.nstripes) {
+                const u32 src = pat_byte(a, pb, p);
+                v[j] = *reinterpret_cast<const uint4 *>(a.in_base[src] + st * a.in_stride +
+                                                        q * 16u);
             }
         }
 #pragma unroll
-        for (int p = 0; p < K; ++p)
-#pragma unroll
-            for (int j = 0; j < TS; ++j)
-                if ((u32)p < k)
-                    *reinterpret_cast<uint4 *>(lds + lds_piece(p, ls + 8u * j, lq, T)) = v[p][j];
+        for (u32 j = 0; j < PER; ++j) {
+            const u32 e = tid + j * NT;
+            const u32 p = e / (T * 32), s = (e / 32) % T, q = e & 31u;
+            if (p < k)
+                *reinterpret_cast<uint4 *>(lds + lds_piece(p, s, q, T)) = v[j];
+        }
     }
     __syncthreads();
 
-    /* compute: (row, 8-stripe subtile) items spread over the 4 waves */
-    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const u32 lane = tid & 63u, cs = lane >> 3, cc = lane & 7u;
+    /* compute: (row, 8-stripe subtile) items spread over the NW waves */
+    const u32 cs = lane >> 3, cc = lane & 7u;
     const u32 items = a.rows * TS;
-    for (u32 it = wave; it < items; it += kBlock / 64) {
+    for (u32 it = wave; it < items; it += NW) {
         const u32 r = it / TS, s = (it % TS) * 8u + cs;
-        u32 acc[8][CW];
+        const u32 rot = (s & 3u) << 6;
+        const uint8_t *col = lds + s * ECD_CHUNK + cc * 8u;
+        /* the row's coefficients: up to 4 words, loaded once into SGPRs */
+        const u32 rw = pb + a.kw * (1 + r);
+        const u32 w0 = a.pat[rw];
+        const u32 w1 = K > 4 ? a.pat[rw + 1] : 0u;
+        const u32 w2 = K > 8 ? a.pat[rw + 2] : 0u;
+        const u32 w3 = K > 12 ? a.pat[rw + 3] : 0u;
+        u32 acc[8][CW], y[8][CW];
 #pragma unroll
         for (int b = 0; b < 8; ++b)
 #pragma unroll
             for (int w = 0; w < CW; ++w)
                 acc[b][w] = 0;
-        const u32 rw = pb + a.kw * (1 + r);
-        for (u32 p = 0; p < k; ++p) {
-            const u32 c = pat_byte(a, rw, p);
-            if (c == 0)
-                continue;
-            u32 y[8][CW];
-            const uint8_t *src = lds + (p * T + s) * ECD_CHUNK + cc * 8u;
+        auto read_input = [&](u32 p, u32 (&d)[8][CW]) {
+            const uint8_t *src = col + p * (T * ECD_CHUNK);
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
-                const uint2 t = *reinterpret_cast<const uint2 *>(src + (((u32)b ^ (s & 3u)) << 6));
-                y[b][0] = t.x;
-                y[b][1] = t.y;
+                const uint2 t = *reinterpret_cast<const uint2 *>(src + (((u32)b << 6) ^ rot));
+                d[b][0] = t.x;
+                d[b][1] = t.y;
             }
-            ecgf::mul_xor_rt<CW>(c, acc, y);
-        }
-        if constexpr (OST) {
-            uint8_t *dst = otile + (r * T + s) * ECD_CHUNK + cc * 8u;
+        };
+        if constexpr (PF)
+            read_input(0, y);
+        for (u32 p = 0; p < k; ++p) {
+            const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
+            const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
+            if constexpr (PF) {
+                /* issue the next input's LDS reads before this multiply */
+                u32 yn[8][CW];
+                read_input(p + 1 < k ? p + 1 : p, yn);
+                ecgf::mul_xor_rt<CW>(c, acc, y);
 #pragma unroll
-            for (int b = 0; b < 8; ++b)
-                *reinterpret_cast<uint2 *>(dst + (((u32)b ^ (s & 3u)) << 6)) =
-                    make_uint2(acc[b][0], acc[b][1]);
-        } else {
-            const uint64_t ost = t0 + s;
-            if (ost < a.nstripes)
-                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
-        }
-    }
-    if constexpr (OST) {
-        /* write the output tile back in 16-byte pieces ordered (stripe, row,
-         * piece): decode output (stripe-major) becomes one contiguous run,
-         * per-row outputs (heal, encode) contiguous 512-byte runs */
-        __syncthreads();
-        const u32 npieces = T * a.rows * (ECD_CHUNK / 16);
-        for (u32 e = tid; e < npieces; e += kBlock) {
-            const u32 q = e & 31u, cr = e >> 5;
-            const u32 s = cr / a.rows, r = cr % a.rows;
-            const uint64_t ost = t0 + s;
-            const uint4 v = *reinterpret_cast<const uint4 *>(otile + ((r * T + s) * ECD_CHUNK) +
-                                                             ((((q >> 2) ^ (s & 3u)) << 6) |
-                                                              ((q & 3u) << 4)));
-            if (ost < a.nstripes) {
-                uint8_t *g = a.out_base[r] + ost * a.out_stride + q * 16u;
-                if constexpr (NTS) {
-                    const v4u w = {v.x, v.y, v.z, v.w};
-                    __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(g));
-                } else {
-                    *reinterpret_cast<uint4 *>(g) = v;
-                }
+                for (int b = 0; b < 8; ++b)
+#pragma unroll
+                    for (int w = 0; w < CW; ++w)
+                        y[b][w] = yn[b][w];
+            } else {
+                if (c == 0)
+                    continue;
+                read_input(p, y);
+                ecgf::mul_xor_rt<CW>(c, acc, y);
             }
         }
+        const uint64_t ost = t0 + s;
+        if (ost < a.nstripes)
+            store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
     }
 }
 
@@ -331,10 +366,10 @@ inline uint64_t combine_grid(uint64_t nstripes)
     return (nstripes + 8 * TS - 1) / (8 * TS);
 }
 
-template <int TS, bool OST>
-inline size_t combine_lds(u32 k, u32 rows)
+template <int TS>
+inline size_t combine_lds(u32 k)
 {
-    return (size_t)(k + (OST ? rows : 0)) * 8 * TS * ECD_CHUNK;
+    return (size_t)k * 8 * TS * ECD_CHUNK;
 }
 
 } // namespace ecdev

@@ -189,18 +189,26 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
         exit(2);
     const double bytes = 2.0 * nst * K * ECD_CHUNK;
     const size_t ob = (size_t)nst * K * ECD_CHUNK;
-    auto add = [&](const char *nm, auto kern, int ts, bool ost) {
-        const size_t lds = (size_t)K * (ost ? 2 : 1) * 8 * ts * ECD_CHUNK;
+    auto add = [&](const char *nm, auto kern, int ts, int nw) {
+        const size_t lds = (size_t)K * 8 * ts * ECD_CHUNK;
         const uint64_t g = (nst + 8 * ts - 1) / (8 * ts);
         vars.push_back({nm, bytes, [=](hipStream_t s) {
-                            hipLaunchKernelGGL(kern, dim3((u32)g), dim3(kBlock), lds, s, a);
+                            hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * nw), lds, s, a);
                         }, out, ob});
     };
-    add("combine TS1", ec_combine<K, 1, false, false, false>, 1, false);
-    add("combine TS2", ec_combine<K, 2, false, false, false>, 2, false);
-    add("combine TS1 OST", ec_combine<K, 1, false, false, true>, 1, true);
-    add("combine TS2 OST", ec_combine<K, 2, false, false, true>, 2, true);
-    add("combine TS1 OST NTS", ec_combine<K, 1, false, true, true>, 1, true);
+    add("TS1 NW4", ec_combine<K, 1, 4, false, false>, 1, 4);
+    add("TS1 NW4 GLDS", ec_combine<K, 1, 4, false, false, true>, 1, 4);
+    add("TS1 NW4 GLDS PF", ec_combine<K, 1, 4, false, false, true, true>, 1, 4);
+    add("TS1 NW8", ec_combine<K, 1, 8, false, false>, 1, 8);
+    add("TS1 NW8 GLDS", ec_combine<K, 1, 8, false, false, true>, 1, 8);
+    add("TS1 NW8 GLDS PF", ec_combine<K, 1, 8, false, false, true, true>, 1, 8);
+    if (K <= 4) {
+        add("TS2 NW4", ec_combine<K, 2, 4, false, false>, 2, 4);
+        add("TS2 NW4 GLDS", ec_combine<K, 2, 4, false, false, true>, 2, 4);
+        add("TS2 NW8", ec_combine<K, 2, 8, false, false>, 2, 8);
+        add("TS2 NW8 GLDS", ec_combine<K, 2, 8, false, false, true>, 2, 8);
+        add("TS2 NW8 GLDS PF", ec_combine<K, 2, 8, false, false, true, true>, 2, 8);
+    }
 }
 
 template <int K, int N, typename KF>
@@ -286,7 +294,81 @@ int main(int argc, char **argv)
         add_decode<8>(v, nst, fr, bufB, c);
         run_group("decode 8+4 dense", v, rounds, iters, s);
     }
-    {   /* encode 4+2, 8+4, 16+4 */
+    {   /* 16+4 decode, dense */
+        const uint64_t nst = user / (16 * ECD_CHUNK);
+        uint8_t *fr[16];
+        for (int p = 0; p < 16; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)(1 + (i * 173 + 11) % 255);
+        std::vector<Variant> v;
+        add_decode<16>(v, nst, fr, bufB, c);
+        run_group("decode 16+4 dense", v, rounds, iters, s);
+    }
+    {   /* 8+4 mixed: 16 random dense patterns over 12 fragments, 1024-stripe groups */
+        const int K = 8, N = 12, NP = 16;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        ecd_combine_desc_t d;
+        memset(&d, 0, sizeof(d));
+        d.k = K;
+        d.rows = K;
+        d.nstripes = nst;
+        d.in_stride = ECD_CHUNK;
+        d.out_stride = (uint64_t)K * ECD_CHUNK;
+        for (int f = 0; f < N; ++f)
+            d.in_base[f] = bufA + (uint64_t)f * nst * ECD_CHUNK * 2 / 3;
+        for (int r = 0; r < K; ++r)
+            d.out_base[r] = bufB + (uint64_t)r * ECD_CHUNK;
+        d.npatterns = NP;
+        d.pat_bytes = K + K * K;
+        uint32_t x = 7;
+        for (int q = 0; q < NP; ++q) {
+            uint8_t *pp = d.pat + q * d.pat_bytes;
+            int used = 0;
+            for (int f = 0; f < N && used < K; ++f) {        /* k of the n bricks */
+                x = x * 1103515245u + 12345u;
+                if ((int)((x >> 16) % (N - f)) < K - used)
+                    pp[used++] = (uint8_t)f;
+            }
+            for (int i = 0; i < K * K; ++i) {
+                x = x * 1103515245u + 12345u;
+                pp[K + i] = (uint8_t)(1 + (x >> 16) % 255);
+            }
+        }
+        const uint64_t ngroups = (nst + 1023) / 1024;
+        std::vector<uint8_t> gp(ngroups);
+        for (auto &g : gp) {
+            x = x * 1103515245u + 12345u;
+            g = (uint8_t)((x >> 16) % NP);
+        }
+        uint8_t *dgp;
+        CHK(hipMalloc(&dgp, ngroups));
+        CHK(hipMemcpy(dgp, gp.data(), ngroups, hipMemcpyHostToDevice));
+        d.group_pattern = dgp;
+        d.group_shift = 10;
+        static CombineArgs a;
+        if (ecdk_pack_args(&d, &a))
+            exit(3);
+        const double bytes = 2.0 * nst * K * ECD_CHUNK;
+        std::vector<Variant> v;
+        const size_t lds = (size_t)K * 8 * ECD_CHUNK;
+        const uint64_t g = (nst + 7) / 8;
+        v.push_back({"mixed TS1 NW4", bytes, [=](hipStream_t st) {
+                         hipLaunchKernelGGL((ec_combine<K, 1, 4, true, false>), dim3((u32)g),
+                                            dim3(256), lds, st, a);
+                     }, bufB, (size_t)nst * K * ECD_CHUNK});
+        v.push_back({"mixed TS1 NW8 GLDS", bytes, [=](hipStream_t st) {
+                         hipLaunchKernelGGL((ec_combine<K, 1, 8, true, false, true>), dim3((u32)g),
+                                            dim3(512), lds, st, a);
+                     }, bufB, (size_t)nst * K * ECD_CHUNK});
+        v.push_back({"mixed TS1 NW8 GLDS PF", bytes, [=](hipStream_t st) {
+                         hipLaunchKernelGGL((ec_combine<K, 1, 8, true, false, true, true>),
+                                            dim3((u32)g), dim3(512), lds, st, a);
+                     }, bufB, (size_t)nst * K * ECD_CHUNK});
+        run_group("decode 8+4 mixed (16 patterns, 1024-stripe groups)", v, rounds, iters, s);
+    }
+    if (getenv("KB_ENCODE")) {   /* encode 4+2, 8+4, 16+4 */
         auto frag_ptrs = [&](uint64_t nst, int n) {
             FragPtrs f;
             for (int i = 0; i < n; ++i)
