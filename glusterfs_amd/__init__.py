@@ -7,10 +7,12 @@ from .ec_method import (  # noqa: F401
     EC_METHOD_CHUNK_SIZE,
     EC_METHOD_MAX_FRAGMENTS,
     ECMatrixList,
+    PinnedArray,
     device_count,
     encode_matrix,
     gf_div,
     gf_mul,
+    host_registered,
     inverse_matrix,
     mask_rows,
     sync_device,

@@ -87,6 +87,8 @@ int ecd_ptr_device(const void *p);
 /* Pinned host allocation helpers (zero-copy PCIe transfers). */
 void *ecd_host_alloc(size_t bytes);
 void ecd_host_free(void *p);
+int ecd_host_register(void *p, size_t bytes);
+int ecd_host_unregister(void *p);
 
 #ifdef __cplusplus
 }

@@ -7,21 +7,26 @@
  * hand over host memory, and the stripe-range partition across all visible
  * MI355X devices (stripes are independent, no collective).
  *
- * Host-memory pipeline per device (two slots, each on its own stream):
- *   slot s:  [pageable only: memcpy user -> pinned]  H2D  kernel  D2H
- *            [pageable only: memcpy pinned -> user after the slot's sync]
- * While one slot's kernel runs, the other slot's copies are in flight (PCIe is
- * full duplex), and the CPU copies of one slot overlap the GPU work of the
- * other.  Pinned user buffers are DMA'd directly with no CPU copy.
+ * Host buffers (the reference codes iobufs in place) are coded
+ * by kernels that read and write pinned host memory directly over PCIe; no
+ * SDMA copies, no device staging.  Pageable buffers bounce through two pinned
+ * slots copied by a CPU thread pool, overlapped with the GPU coding the other
+ * slot.  See "host-buffer pipeline" below for the measurements behind this.
  */
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -33,7 +38,28 @@
 namespace {
 
 constexpr int kMaxDev = 16;
-constexpr uint64_t kBatchBytes = 32ull << 20; /* input bytes per pipeline batch */
+/* Stripes per pipeline batch are sized to this many input bytes; the
+ * EC_PIPE_BATCH_MB / EC_COPY_THREADS environment overrides exist for tuning
+ * (tools/kbench/e2e.c). */
+uint64_t pipe_batch_bytes()
+{
+    static const uint64_t v = [] {
+        const char *e = getenv("EC_PIPE_BATCH_MB");
+        const long mb = e ? atol(e) : 0;
+        return (uint64_t)(mb > 0 && mb <= 1024 ? mb : 32) << 20;
+    }();
+    return v;
+}
+
+int copy_threads()
+{
+    static const int v = [] {
+        const char *e = getenv("EC_COPY_THREADS");
+        const int t = e ? atoi(e) : 8;
+        return std::min(std::max(t, 0), 64);
+    }();
+    return v;
+}
 
 std::mutex g_err_mu;
 std::string g_err;
@@ -81,71 +107,171 @@ hipStream_t pick_stream(void *stream)
     return stream ? static_cast<hipStream_t>(stream) : hipStreamPerThread;
 }
 
-/* Device-resident staging for one pipeline slot pair; pooled per device. */
+/* ------------------------------------------------- host-buffer pipeline */
+
+/* Host buffers never go through SDMA copies here: the coding kernels read
+ * and write pinned host memory directly over PCIe.  Measured on MI355X with
+ * tools/kbench/zerocopy.hip, CU-issued accesses move ~56 GB/s host->device,
+ * ~55 GB/s device->host and ~45 GB/s EACH WAY when a kernel does both at once
+ * (~90 GB/s bidirectional), while SDMA copies chained behind kernels through
+ * cross-stream events reached only 45-65 GB/s in total and stalled the
+ * enqueueing thread (tools/kbench/e2e.c, EC_PIPE_TRACE).  So:
+ *   - pinned (page-locked, device-mapped) caller buffers are coded in place:
+ *     one kernel per batch, no copies at all;
+ *   - pageable caller buffers are staged through two pinned slots by a pool
+ *     of CPU threads: batch b's input copy and batch b-1's output copy run
+ *     on the CPU while the GPU codes batch b from the other slot. */
+
+/* Pool of CPU threads for staging copies (shared by all devices/callers). */
+class CopyPool {
+  public:
+    struct Piece {
+        uint8_t *dst;
+        const uint8_t *src;
+        size_t n;
+    };
+
+    void run(const std::vector<Piece> &pieces)
+    {
+        if (pieces.empty())
+            return;
+        start();
+        Job j;
+        j.p = &pieces;
+        if (!th_.empty() && pieces.size() > 1) {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(&j);
+            cv_.notify_all();
+        }
+        work(j);
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [&] { return j.done.load() == pieces.size() && j.active == 0; });
+        for (auto it = q_.begin(); it != q_.end(); ++it)
+            if (*it == &j) {
+                q_.erase(it);
+                break;
+            }
+    }
+
+    ~CopyPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+            cv_.notify_all();
+        }
+        for (auto &t : th_)
+            t.join();
+    }
+
+  private:
+    struct Job {
+        const std::vector<Piece> *p;
+        std::atomic<size_t> next{0}, done{0};
+        int active = 0; /* workers inside work(); guarded by mu_ */
+    };
+
+    void start()
+    {
+        std::call_once(once_, [this] {
+            for (int i = 0; i < copy_threads(); ++i)
+                th_.emplace_back([this] { loop(); });
+        });
+    }
+
+    void work(Job &j)
+    {
+        const std::vector<Piece> &p = *j.p;
+        for (size_t i; (i = j.next.fetch_add(1)) < p.size();) {
+            memcpy(p[i].dst, p[i].src, p[i].n);
+            j.done.fetch_add(1);
+        }
+    }
+
+    void loop()
+    {
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+            if (stop_)
+                return;
+            Job *j = q_.front();
+            q_.pop_front(); /* claimed pieces are tracked by the job itself */
+            ++j->active;
+            g.unlock();
+            work(*j);
+            g.lock();
+            --j->active;
+            done_cv_.notify_all();
+        }
+    }
+
+    std::once_flag once_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<Job *> q_;
+    std::vector<std::thread> th_;
+    bool stop_ = false;
+};
+
+CopyPool g_copy_pool;
+
+/* Split [dst, src, n) copies into ~2 MiB pieces for the pool. */
+void add_copy(std::vector<CopyPool::Piece> &v, uint8_t *dst, const uint8_t *src, size_t n)
+{
+    constexpr size_t kPiece = 2u << 20;
+    for (size_t o = 0; o < n; o += kPiece)
+        v.push_back({dst + o, src + o, std::min(kPiece, n - o)});
+}
+
+/* Device-visible address of [p, p+n) when it lies in pinned, device-mapped
+ * host memory (hipHostMalloc / ec_method_host_alloc / hipHostRegister),
+ * else nullptr.  16-byte alignment is required for the kernels' vector
+ * accesses. */
+uint8_t *mapped(const void *p, size_t n)
+{
+    if (!p || ((uintptr_t)p & 15))
+        return nullptr;
+    void *d0 = nullptr, *d1 = nullptr;
+    if (hipHostGetDevicePointer(&d0, const_cast<void *>(p), 0) != hipSuccess ||
+        (n > 1 && hipHostGetDevicePointer(&d1, (uint8_t *)p + n - 1, 0) != hipSuccess)) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    /* one contiguous mapping, at the same address on both sides (ROCm maps
+     * pinned host memory at its host virtual address) */
+    if (d0 != p || (n > 1 && (uint8_t *)d1 != (uint8_t *)d0 + n - 1))
+        return nullptr;
+    return static_cast<uint8_t *>(d0);
+}
+
+/* Per-device pipeline resources (pooled). */
+constexpr int kSlots = 2;
+
 struct Stage {
     int dev = -1;
-    hipStream_t st[2] = {nullptr, nullptr};
-    uint8_t *din[2] = {nullptr, nullptr};
-    uint8_t *dout[2] = {nullptr, nullptr};
-    uint8_t *dgrp[2] = {nullptr, nullptr};
-    uint8_t *pin_in[2] = {nullptr, nullptr};
-    uint8_t *pin_out[2] = {nullptr, nullptr};
-    uint8_t *pin_grp[2] = {nullptr, nullptr};
+    hipStream_t stream = nullptr;
+    hipEvent_t done[kSlots] = {};
+    uint8_t *pin_in[kSlots] = {}, *pin_out[kSlots] = {}, *pin_grp[kSlots] = {};
     size_t cap_in = 0, cap_out = 0, cap_grp = 0;
-    bool pinned_staging = false;
 };
 
 std::mutex g_pool_mu;
 std::vector<Stage *> g_pool[kMaxDev];
 
-void free_bufs(Stage *s)
+int grow(uint8_t *(&slot)[kSlots], size_t &cap, size_t want)
 {
-    for (int i = 0; i < 2; ++i) {
-        if (s->din[i])
-            (void)hipFree(s->din[i]);
-        if (s->dout[i])
-            (void)hipFree(s->dout[i]);
-        if (s->dgrp[i])
-            (void)hipFree(s->dgrp[i]);
-        if (s->pin_in[i])
-            (void)hipHostFree(s->pin_in[i]);
-        if (s->pin_out[i])
-            (void)hipHostFree(s->pin_out[i]);
-        if (s->pin_grp[i])
-            (void)hipHostFree(s->pin_grp[i]);
-        s->din[i] = s->dout[i] = s->dgrp[i] = nullptr;
-        s->pin_in[i] = s->pin_out[i] = s->pin_grp[i] = nullptr;
-    }
-    s->cap_in = s->cap_out = s->cap_grp = 0;
-    s->pinned_staging = false;
-}
-
-int ensure(Stage *s, size_t in, size_t out, size_t grp, bool need_pinned)
-{
-    if (in <= s->cap_in && out <= s->cap_out && grp <= s->cap_grp &&
-        (!need_pinned || s->pinned_staging))
+    if (want <= cap)
         return 0;
-    HIPCHK(hipStreamSynchronize(s->st[0]));
-    HIPCHK(hipStreamSynchronize(s->st[1]));
-    in = std::max(in, s->cap_in);
-    out = std::max(out, s->cap_out);
-    grp = std::max<size_t>(std::max(grp, s->cap_grp), 64);
-    need_pinned = need_pinned || s->pinned_staging;
-    free_bufs(s);
-    for (int i = 0; i < 2; ++i) {
-        HIPCHK(hipMalloc(&s->din[i], in));
-        HIPCHK(hipMalloc(&s->dout[i], out));
-        HIPCHK(hipMalloc(&s->dgrp[i], grp));
-        HIPCHK(hipHostMalloc(&s->pin_grp[i], grp, hipHostMallocDefault));
-        if (need_pinned) {
-            HIPCHK(hipHostMalloc(&s->pin_in[i], in, hipHostMallocDefault));
-            HIPCHK(hipHostMalloc(&s->pin_out[i], out, hipHostMallocDefault));
+    for (auto &p : slot)
+        if (p) {
+            (void)hipHostFree(p);
+            p = nullptr;
         }
-    }
-    s->cap_in = in;
-    s->cap_out = out;
-    s->cap_grp = grp;
-    s->pinned_staging = need_pinned;
+    cap = 0;
+    for (auto &p : slot)
+        HIPCHK(hipHostMalloc(&p, want, hipHostMallocDefault));
+    cap = want;
     return 0;
 }
 
@@ -161,9 +287,12 @@ Stage *acquire(int dev)
     }
     Stage *s = new Stage;
     s->dev = dev;
-    if (hipSetDevice(g_dev_ids[dev]) != hipSuccess ||
-        hipStreamCreateWithFlags(&s->st[0], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&s->st[1], hipStreamNonBlocking) != hipSuccess) {
+    bool ok = hipSetDevice(g_dev_ids[dev]) == hipSuccess &&
+              hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; ok && i < kSlots; ++i)
+        ok = hipEventCreateWithFlags(&s->done[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
         delete s;
         return nullptr;
     }
@@ -176,23 +305,76 @@ void release(Stage *s)
     g_pool[s->dev].push_back(s);
 }
 
-bool is_pinned_host(const void *p)
+/* One caller buffer region of a batch.  `kptr` is what the kernel uses:
+ * the caller's own (mapped) memory, or `pin_off` inside the slot's pinned
+ * staging buffer when the caller's memory is pageable. */
+struct Region {
+    uint8_t *host;
+    size_t n;
+    bool staged;
+    size_t pin_off;
+};
+
+struct Batch {
+    std::vector<Region> in, out;
+    std::function<int(hipStream_t)> launch;
+};
+
+/* Run `nbatches` batches: make(b, slot, batch) describes batch b's regions
+ * and its launch (which reads kernel addresses from the regions' slots). */
+int run_pipeline(Stage *s, uint64_t nbatches,
+                 const std::function<int(uint64_t, int, Batch &)> &make)
 {
-    if (!p)
-        return false;
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
+    int rc = 0;
+    Batch prev;
+    int prev_slot = -1;
+    auto ok = [&](hipError_t e) {
+        if (e != hipSuccess && rc == 0) {
+            set_err("pipeline", e);
+            rc = -EIO;
+        }
+        return rc == 0;
+    };
+    auto drain = [&]() {
+        /* wait for the previous batch and copy its staged outputs back */
+        if (prev_slot < 0)
+            return;
+        if (ok(hipEventSynchronize(s->done[prev_slot]))) {
+            std::vector<CopyPool::Piece> pc;
+            for (const Region &r : prev.out)
+                if (r.staged)
+                    add_copy(pc, r.host, s->pin_out[prev_slot] + r.pin_off, r.n);
+            g_copy_pool.run(pc);
+        }
+        prev_slot = -1;
+    };
+    for (uint64_t b = 0; rc == 0 && b < nbatches; ++b) {
+        const int slot = (int)(b % kSlots); /* free: batch b-2 was drained */
+        Batch bt;
+        if ((rc = make(b, slot, bt)) != 0)
+            break;
+        std::vector<CopyPool::Piece> pc;
+        for (const Region &r : bt.in)
+            if (r.staged)
+                add_copy(pc, s->pin_in[slot] + r.pin_off, r.host, r.n);
+        g_copy_pool.run(pc);
+        if ((rc = bt.launch(s->stream)) != 0 || !ok(hipEventRecord(s->done[slot], s->stream)))
+            break;
+        drain();
+        prev = std::move(bt);
+        prev_slot = slot;
     }
-    return a.type == hipMemoryTypeHost;
+    drain();
+    ok(hipStreamSynchronize(s->stream));
+    return rc;
 }
 
-/* Copy helper that tolerates our own pinned staging or a pinned user buffer. */
-void copy_bytes(void *dst, const void *src, size_t n)
+/* Kernel address of a region of the current batch. */
+inline uint8_t *kaddr(const Stage *s, int slot, const Region &r, bool out)
 {
-    if (n)
-        memcpy(dst, src, n);
+    if (!r.staged)
+        return r.host; /* mapped: device address == host address (checked) */
+    return (out ? s->pin_out[slot] : s->pin_in[slot]) + r.pin_off;
 }
 
 /* ---------------------------------------------------------------- encode */
@@ -205,14 +387,11 @@ struct EncodeJob {
     uint64_t s0, s1;        /* stripe range of this device                */
 };
 
-int launch_encode(hipStream_t st, const EncodeJob &j, const uint8_t *din, uint8_t *dout,
-                  uint64_t cnt, uint64_t batch_stripes)
+int launch_encode(hipStream_t st, const EncodeJob &j, const uint8_t *din, uint8_t *const *outs,
+                  uint64_t cnt)
 {
-    void *outs[ECD_MAX_ROWS];
-    for (uint32_t i = 0; i < j.n; ++i)
-        outs[i] = dout + (uint64_t)i * batch_stripes * ECD_CHUNK;
     if (ecdk_has_vander(j.k, j.n))
-        return ecdk_encode_vander(st, j.k, j.n, cnt, din, outs);
+        return ecdk_encode_vander(st, j.k, j.n, cnt, din, (void *const *)outs);
     ecd_combine_desc_t d;
     memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
     d.k = j.k;
@@ -235,71 +414,40 @@ int run_encode_dev(int dev, const EncodeJob &j)
     if (j.s1 <= j.s0)
         return 0;
     HIPCHK(hipSetDevice(g_dev_ids[dev]));
-    const uint64_t stripe_in = (uint64_t)j.k * ECD_CHUNK;
-    const uint64_t B = std::max<uint64_t>(1, kBatchBytes / stripe_in);
-    const bool pin_in = is_pinned_host(j.in);
-    bool pin_out = true;
-    for (uint32_t i = 0; i < j.n && pin_out; ++i)
-        pin_out = is_pinned_host(j.out[i]);
-    const bool staged = !(pin_in && pin_out);
-
+    const uint64_t stripe_in = (uint64_t)j.k * ECD_CHUNK, cnt_all = j.s1 - j.s0;
+    const bool in_direct = mapped(j.in + j.s0 * stripe_in, cnt_all * stripe_in) != nullptr;
+    bool out_direct[ECD_MAX_ROWS], all_direct = in_direct;
+    for (uint32_t i = 0; i < j.n; ++i) {
+        out_direct[i] = mapped(j.out[i] + j.s0 * ECD_CHUNK, cnt_all * ECD_CHUNK) != nullptr;
+        all_direct &= out_direct[i];
+    }
+    /* fully mapped jobs still run in batches so one launch stays short */
+    const uint64_t B = std::max<uint64_t>(
+        1, (all_direct ? 8 : 1) * pipe_batch_bytes() / stripe_in);
     Stage *s = acquire(dev);
     if (!s)
         return -EIO;
-    int rc = ensure(s, B * stripe_in, B * j.n * ECD_CHUNK, 0, staged);
-    uint64_t pend_start[2] = {0, 0}, pend_cnt[2] = {0, 0};
-    int it = 0;
-    for (uint64_t a = j.s0; rc == 0 && a < j.s1; a += B, ++it) {
-        const int sl = it & 1;
-        const uint64_t cnt = std::min(B, j.s1 - a);
-        hipStream_t st = s->st[sl];
-        if (staged) {
-            if (hipStreamSynchronize(st) != hipSuccess) {
-                rc = -EIO;
-                break;
-            }
-            if (pend_cnt[sl] && !pin_out) {
-                for (uint32_t i = 0; i < j.n; ++i)
-                    copy_bytes(j.out[i] + pend_start[sl] * ECD_CHUNK,
-                               s->pin_out[sl] + (uint64_t)i * B * ECD_CHUNK,
-                               pend_cnt[sl] * ECD_CHUNK);
-            }
-            pend_cnt[sl] = 0;
-        }
-        const uint8_t *src = j.in + a * stripe_in;
-        if (!pin_in) {
-            copy_bytes(s->pin_in[sl], src, cnt * stripe_in);
-            src = s->pin_in[sl];
-        }
-        if (hipMemcpyAsync(s->din[sl], src, cnt * stripe_in, hipMemcpyHostToDevice, st) !=
-            hipSuccess) {
-            rc = -EIO;
-            break;
-        }
-        rc = launch_encode(st, j, s->din[sl], s->dout[sl], cnt, B);
-        if (rc)
-            break;
-        for (uint32_t i = 0; i < j.n; ++i) {
-            uint8_t *dst = pin_out ? j.out[i] + a * ECD_CHUNK
-                                   : s->pin_out[sl] + (uint64_t)i * B * ECD_CHUNK;
-            if (hipMemcpyAsync(dst, s->dout[sl] + (uint64_t)i * B * ECD_CHUNK,
-                               cnt * ECD_CHUNK, hipMemcpyDeviceToHost, st) != hipSuccess) {
-                rc = -EIO;
-                break;
-            }
-        }
-        pend_start[sl] = a;
-        pend_cnt[sl] = cnt;
-    }
-    for (int sl = 0; sl < 2; ++sl) {
-        if (hipStreamSynchronize(s->st[sl]) != hipSuccess)
-            rc = rc ? rc : -EIO;
-        if (rc == 0 && pend_cnt[sl] && !pin_out)
+    int rc = grow(s->pin_in, s->cap_in, in_direct ? 0 : B * stripe_in);
+    if (rc == 0)
+        rc = grow(s->pin_out, s->cap_out, all_direct ? 0 : B * j.n * ECD_CHUNK);
+    const uint64_t nb = (cnt_all + B - 1) / B;
+    if (rc == 0)
+        rc = run_pipeline(s, nb, [&](uint64_t b, int slot, Batch &bt) {
+            const uint64_t a = j.s0 + b * B, cnt = std::min(B, j.s1 - a);
+            bt.in.push_back({const_cast<uint8_t *>(j.in) + a * stripe_in, cnt * stripe_in,
+                             !in_direct, 0});
             for (uint32_t i = 0; i < j.n; ++i)
-                copy_bytes(j.out[i] + pend_start[sl] * ECD_CHUNK,
-                           s->pin_out[sl] + (uint64_t)i * B * ECD_CHUNK,
-                           pend_cnt[sl] * ECD_CHUNK);
-    }
+                bt.out.push_back({j.out[i] + a * ECD_CHUNK, cnt * ECD_CHUNK, !out_direct[i],
+                                  (size_t)i * B * ECD_CHUNK});
+            const uint8_t *din = kaddr(s, slot, bt.in[0], false);
+            std::vector<uint8_t *> outs(j.n);
+            for (uint32_t i = 0; i < j.n; ++i)
+                outs[i] = kaddr(s, slot, bt.out[i], true);
+            bt.launch = [&j, din, outs, cnt](hipStream_t st) {
+                return launch_encode(st, j, din, outs.data(), cnt);
+            };
+            return 0;
+        });
     release(s);
     return rc;
 }
@@ -316,139 +464,89 @@ struct DecodeJob {
     uint64_t s0, s1;
 };
 
-/* Device output layout of one batch: stripe-major data (outs == NULL) or
- * one B-stripe region per row (outs != NULL). */
-void flush_decode(const DecodeJob &j, const uint8_t *pin, uint64_t a, uint64_t cnt, uint64_t B)
-{
-    if (j.outs) {
-        for (uint32_t r = 0; r < j.rows; ++r)
-            copy_bytes(j.outs[r] + a * ECD_CHUNK, pin + (uint64_t)r * B * ECD_CHUNK,
-                       cnt * ECD_CHUNK);
-    } else {
-        copy_bytes(j.out + a * (uint64_t)j.rows * ECD_CHUNK, pin,
-                   cnt * (uint64_t)j.rows * ECD_CHUNK);
-    }
-}
-
 int run_decode_dev(int dev, const DecodeJob &j)
 {
     if (j.s1 <= j.s0)
         return 0;
     HIPCHK(hipSetDevice(g_dev_ids[dev]));
-    const uint64_t out_stripe = (uint64_t)j.rows * ECD_CHUNK;
-    uint64_t B = std::max<uint64_t>(1, kBatchBytes / ((uint64_t)j.nfrags * ECD_CHUNK));
+    const uint64_t out_stripe = (uint64_t)j.rows * ECD_CHUNK, cnt_all = j.s1 - j.s0;
+    bool in_direct[ECD_MAX_ROWS] = {}, out_direct[ECD_MAX_ROWS] = {}, all_direct = true;
+    bool any_in_staged = false;
+    for (uint32_t f = 0; f < j.nfrags; ++f)
+        if (j.frags[f]) {
+            in_direct[f] = mapped(j.frags[f] + j.s0 * ECD_CHUNK, cnt_all * ECD_CHUNK) != nullptr;
+            all_direct &= in_direct[f];
+            any_in_staged |= !in_direct[f];
+        }
+    if (j.outs) {
+        for (uint32_t r = 0; r < j.rows; ++r) {
+            out_direct[r] = mapped(j.outs[r] + j.s0 * ECD_CHUNK, cnt_all * ECD_CHUNK) != nullptr;
+            all_direct &= out_direct[r];
+        }
+    } else {
+        out_direct[0] = mapped(j.out + j.s0 * out_stripe, cnt_all * out_stripe) != nullptr;
+        all_direct &= out_direct[0];
+    }
+    uint64_t B = std::max<uint64_t>(
+        1, (all_direct ? 8 : 1) * pipe_batch_bytes() / ((uint64_t)j.nfrags * ECD_CHUNK));
     const uint64_t grp = j.group_pattern ? (1ull << j.group_shift) : 1;
     if (j.group_pattern)
         B = std::max<uint64_t>(grp, B / grp * grp);
-    const uint64_t ngrp_max = j.group_pattern ? B / grp + 1 : 0;
-    bool pin_in = true;
-    for (uint32_t f = 0; f < j.nfrags && pin_in; ++f)
-        pin_in = is_pinned_host(j.frags[f]);
-    bool pin_out = true;
-    if (j.outs) {
-        for (uint32_t r = 0; r < j.rows && pin_out; ++r)
-            pin_out = is_pinned_host(j.outs[r]);
-    } else {
-        pin_out = is_pinned_host(j.out);
-    }
-    const bool staged = !(pin_in && pin_out);
-
     Stage *s = acquire(dev);
     if (!s)
         return -EIO;
-    int rc = ensure(s, B * j.nfrags * ECD_CHUNK, B * out_stripe, ngrp_max, staged);
-    uint64_t pend_start[2] = {0, 0}, pend_cnt[2] = {0, 0};
-    int it = 0;
-    for (uint64_t a = j.s0; rc == 0 && a < j.s1; a += B, ++it) {
-        const int sl = it & 1;
-        const uint64_t cnt = std::min(B, j.s1 - a);
-        hipStream_t st = s->st[sl];
-        if (hipStreamSynchronize(st) != hipSuccess) {
-            rc = -EIO;
-            break;
-        }
-        if (pend_cnt[sl] && !pin_out)
-            flush_decode(j, s->pin_out[sl], pend_start[sl], pend_cnt[sl], B);
-        pend_cnt[sl] = 0;
-
-        for (uint32_t f = 0; f < j.nfrags && rc == 0; ++f) {
-            if (!j.frags[f])
-                continue;
-            const uint8_t *src = j.frags[f] + a * ECD_CHUNK;
-            uint8_t *dst = s->din[sl] + (uint64_t)f * B * ECD_CHUNK;
-            if (!pin_in) {
-                uint8_t *pin = s->pin_in[sl] + (uint64_t)f * B * ECD_CHUNK;
-                copy_bytes(pin, src, cnt * ECD_CHUNK);
-                src = pin;
+    int rc = grow(s->pin_in, s->cap_in, any_in_staged ? B * j.nfrags * ECD_CHUNK : 0);
+    if (rc == 0)
+        rc = grow(s->pin_out, s->cap_out, all_direct ? 0 : B * out_stripe);
+    if (rc == 0)
+        rc = grow(s->pin_grp, s->cap_grp, j.group_pattern ? B / grp + 1 : 0);
+    const uint64_t nb = (cnt_all + B - 1) / B;
+    if (rc == 0)
+        rc = run_pipeline(s, nb, [&](uint64_t b, int slot, Batch &bt) {
+            const uint64_t a = j.s0 + b * B, cnt = std::min(B, j.s1 - a);
+            auto d = std::make_shared<ecd_combine_desc_t>();
+            memset(d.get(), 0, offsetof(ecd_combine_desc_t, pat));
+            d->k = j.k;
+            d->rows = j.rows;
+            d->nstripes = cnt;
+            d->in_stride = ECD_CHUNK;
+            for (uint32_t f = 0; f < j.nfrags; ++f) {
+                if (!j.frags[f])
+                    continue;
+                bt.in.push_back({const_cast<uint8_t *>(j.frags[f]) + a * ECD_CHUNK,
+                                 cnt * ECD_CHUNK, !in_direct[f], (size_t)f * B * ECD_CHUNK});
+                d->in_base[f] = kaddr(s, slot, bt.in.back(), false);
             }
-            if (hipMemcpyAsync(dst, src, cnt * ECD_CHUNK, hipMemcpyHostToDevice, st) !=
-                hipSuccess)
-                rc = -EIO;
-        }
-        if (rc)
-            break;
-
-        ecd_combine_desc_t d;
-        memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
-        d.k = j.k;
-        d.rows = j.rows;
-        d.nstripes = cnt;
-        d.in_stride = ECD_CHUNK;
-        for (uint32_t f = 0; f < j.nfrags; ++f)
-            d.in_base[f] = s->din[sl] + (uint64_t)f * B * ECD_CHUNK;
-        if (j.outs) {
-            d.out_stride = ECD_CHUNK;
-            for (uint32_t r = 0; r < j.rows; ++r)
-                d.out_base[r] = s->dout[sl] + (uint64_t)r * B * ECD_CHUNK;
-        } else {
-            d.out_stride = out_stripe;
-            for (uint32_t r = 0; r < j.rows; ++r)
-                d.out_base[r] = s->dout[sl] + (uint64_t)r * ECD_CHUNK;
-        }
-        d.npatterns = j.npatterns;
-        d.pat_bytes = j.k + j.rows * j.k;
-        memcpy(d.pat, j.pats, (size_t)j.npatterns * d.pat_bytes);
-        if (j.group_pattern) {
-            /* a is a multiple of the group size (B is, and s0 is aligned) */
-            const uint64_t g0 = a >> j.group_shift;
-            const uint64_t gn = (cnt + grp - 1) >> j.group_shift;
-            memcpy(s->pin_grp[sl], j.group_pattern + g0, gn);
-            if (hipMemcpyAsync(s->dgrp[sl], s->pin_grp[sl], gn, hipMemcpyHostToDevice, st) !=
-                hipSuccess) {
-                rc = -EIO;
-                break;
+            if (j.outs) {
+                d->out_stride = ECD_CHUNK;
+                for (uint32_t r = 0; r < j.rows; ++r) {
+                    bt.out.push_back({j.outs[r] + a * ECD_CHUNK, cnt * ECD_CHUNK,
+                                      !out_direct[r], (size_t)r * B * ECD_CHUNK});
+                    d->out_base[r] = kaddr(s, slot, bt.out.back(), true);
+                }
+            } else {
+                d->out_stride = out_stripe;
+                bt.out.push_back({j.out + a * out_stripe, cnt * out_stripe, !out_direct[0], 0});
+                uint8_t *o = kaddr(s, slot, bt.out.back(), true);
+                for (uint32_t r = 0; r < j.rows; ++r)
+                    d->out_base[r] = o + (uint64_t)r * ECD_CHUNK;
             }
-            d.group_pattern = s->dgrp[sl];
-            d.group_shift = j.group_shift;
-        }
-        rc = ecdk_combine(st, &d);
-        if (rc)
-            break;
-        if (j.outs) {
-            for (uint32_t r = 0; r < j.rows && rc == 0; ++r) {
-                uint8_t *dst = pin_out ? j.outs[r] + a * ECD_CHUNK
-                                       : s->pin_out[sl] + (uint64_t)r * B * ECD_CHUNK;
-                if (hipMemcpyAsync(dst, s->dout[sl] + (uint64_t)r * B * ECD_CHUNK,
-                                   cnt * ECD_CHUNK, hipMemcpyDeviceToHost, st) != hipSuccess)
-                    rc = -EIO;
+            d->npatterns = j.npatterns;
+            d->pat_bytes = j.k + j.rows * j.k;
+            memcpy(d->pat, j.pats, (size_t)j.npatterns * d->pat_bytes);
+            if (j.group_pattern) {
+                /* a is a multiple of the group size (B is, and s0 is aligned);
+                 * the kernel reads the group-map slice from the slot's pinned
+                 * buffer (free: its previous batch has been drained) */
+                const uint64_t g0 = a >> j.group_shift;
+                const uint64_t gn = (cnt + grp - 1) >> j.group_shift;
+                memcpy(s->pin_grp[slot], j.group_pattern + g0, gn);
+                d->group_pattern = s->pin_grp[slot];
+                d->group_shift = j.group_shift;
             }
-        } else {
-            uint8_t *dst = pin_out ? j.out + a * out_stripe : s->pin_out[sl];
-            if (hipMemcpyAsync(dst, s->dout[sl], cnt * out_stripe, hipMemcpyDeviceToHost,
-                               st) != hipSuccess)
-                rc = -EIO;
-        }
-        if (rc)
-            break;
-        pend_start[sl] = a;
-        pend_cnt[sl] = cnt;
-    }
-    for (int sl = 0; sl < 2; ++sl) {
-        if (hipStreamSynchronize(s->st[sl]) != hipSuccess)
-            rc = rc ? rc : -EIO;
-        if (rc == 0 && pend_cnt[sl] && !pin_out)
-            flush_decode(j, s->pin_out[sl], pend_start[sl], pend_cnt[sl], B);
-    }
+            bt.launch = [d](hipStream_t st) { return ecdk_combine(st, d.get()); };
+            return 0;
+        });
     release(s);
     return rc;
 }
@@ -614,6 +712,32 @@ void ecd_host_free(void *p)
 {
     if (p)
         (void)hipHostFree(p);
+}
+
+int ecd_host_register(void *p, size_t bytes)
+{
+    if (ecd_device_count() == 0)
+        return -ENODEV;
+    if (!p || bytes == 0)
+        return -EINVAL;
+    const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped);
+    if (e != hipSuccess) {
+        set_err("hipHostRegister", e);
+        return e == hipErrorHostMemoryAlreadyRegistered ? -EEXIST : -ENOMEM;
+    }
+    return 0;
+}
+
+int ecd_host_unregister(void *p)
+{
+    if (ecd_device_count() == 0)
+        return -ENODEV;
+    const hipError_t e = hipHostUnregister(p);
+    if (e != hipSuccess) {
+        set_err("hipHostUnregister", e);
+        return -EINVAL;
+    }
+    return 0;
 }
 
 } /* extern "C" */

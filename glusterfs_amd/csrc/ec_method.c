@@ -415,6 +415,18 @@ ec_method_host_free(void *p)
     ecd_host_free(p);
 }
 
+int32_t
+ec_method_host_register(void *p, size_t bytes)
+{
+    return ecd_host_register(p, bytes);
+}
+
+int32_t
+ec_method_host_unregister(void *p)
+{
+    return ecd_host_unregister(p);
+}
+
 static const char *const ecm_known_gens[] = {"none", "auto", "x64", "sse", "avx", "hip",
                                              NULL};
 

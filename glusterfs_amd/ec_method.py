@@ -33,6 +33,7 @@ EXPORTS = (
     "ec_method_decode_device", "ec_method_decode_mixed_device",
     "ec_method_heal_device", "ec_method_sync_device", "ec_method_device_count",
     "ec_method_last_error", "ec_method_host_alloc", "ec_method_host_free",
+    "ec_method_host_register", "ec_method_host_unregister",
     "ec_method_encode_matrix", "ec_method_inverse_matrix", "ec_method_gf_mul",
     "ec_method_gf_div",
 )
@@ -97,6 +98,8 @@ def _load():
         "ec_method_last_error": (ctypes.c_char_p, []),
         "ec_method_host_alloc": (vp, [ctypes.c_size_t]),
         "ec_method_host_free": (None, [vp]),
+        "ec_method_host_register": (ctypes.c_int32, [vp, ctypes.c_size_t]),
+        "ec_method_host_unregister": (ctypes.c_int32, [vp]),
         "ec_method_encode_matrix": (i32, [u32, u32, vp]),
         "ec_method_inverse_matrix": (i32, [u32, vp, vp]),
         "ec_method_gf_mul": (u32, [u32, u32]),
@@ -139,6 +142,51 @@ def _check(rc, what):
 
 def device_count():
     return lib.ec_method_device_count()
+
+
+class PinnedArray:
+    """numpy uint8 view of pinned, device-mapped host memory
+    (ec_method_host_alloc): host buffers here are coded in place over PCIe."""
+
+    def __init__(self, nbytes):
+        import numpy as np
+        self.nbytes = int(nbytes)
+        self.ptr = lib.ec_method_host_alloc(max(1, self.nbytes))
+        if not self.ptr:
+            raise MemoryError("ec_method_host_alloc(%d)" % self.nbytes)
+        raw = (ctypes.c_uint8 * max(1, self.nbytes)).from_address(self.ptr)
+        self.array = np.ctypeslib.as_array(raw)[:self.nbytes]
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            lib.ec_method_host_free(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self.array
+
+    def __exit__(self, *exc):
+        self.free()
+
+    def __del__(self):
+        self.free()
+
+
+class host_registered:
+    """Context manager pinning an existing host buffer (ec_method_host_register)."""
+
+    def __init__(self, buf):
+        self.buf = buf
+        self.ptr = addr(buf)
+        self.nbytes = buf.nbytes
+
+    def __enter__(self):
+        _check(lib.ec_method_host_register(self.ptr, self.nbytes), "ec_method_host_register")
+        return self.buf
+
+    def __exit__(self, *exc):
+        _check(lib.ec_method_host_unregister(self.ptr), "ec_method_host_unregister")
 
 
 def gf_mul(a, b):

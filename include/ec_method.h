@@ -161,9 +161,16 @@ int32_t ec_method_sync_device(int device, void *stream);
 int32_t ec_method_device_count(void);
 /* Last device-layer error string (diagnostics). */
 const char *ec_method_last_error(void);
-/* Pinned host memory for zero-copy PCIe transfers. */
+/* Pinned, device-mapped host memory.  Host buffers in such memory (16-byte
+ * aligned) are coded in place by the GPU over PCIe with no staging copy;
+ * pageable buffers are staged through pinned slots by CPU threads. */
 void *ec_method_host_alloc(size_t bytes);
 void ec_method_host_free(void *p);
+/* Pin and map an existing host range (e.g. a GlusterFS iobuf arena, see
+ * INTEGRATION.md) so buffers inside it take the zero-copy path.  Returns 0
+ * or -errno.  Unregister before freeing the memory. */
+int32_t ec_method_host_register(void *p, size_t bytes);
+int32_t ec_method_host_unregister(void *p);
 
 /* Host-side matrix helpers, exported for tests and tools: the n x k encode
  * matrix (ec-method.c:22-36) and the k x k inverse for ascending rows

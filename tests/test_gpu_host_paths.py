@@ -1,0 +1,153 @@
+"""GPU parity of the host-buffer paths (ec_device.hip "host-buffer pipeline").
+
+Host buffers are either coded in place over PCIe (pinned, device-mapped,
+16-byte aligned) or staged through pinned slots by CPU threads (pageable or
+misaligned); one call may mix both kinds.  Sizes span several pipeline
+batches (32 MiB staged, 256 MiB in place) so slot rotation and ragged final
+batches are exercised.  Bit-exact against the CPU oracle.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CHUNK = 512
+
+
+@pytest.fixture(scope="module")
+def ec():
+    import glusterfs_amd as g
+    if g.device_count() < 1:
+        pytest.fail("no MI355X visible: the product has no CPU path")
+    return g
+
+
+def rand_bytes(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
+
+
+class Bufs:
+    """Allocates host buffers of one kind: 'pinned', 'pageable',
+    'misaligned' (pinned + 8 bytes: must fall back to staging) or
+    'registered' (pageable pinned through ec_method_host_register)."""
+
+    def __init__(self, ec, kind):
+        self.ec, self.kind, self.keep, self.regs = ec, kind, [], []
+
+    def new(self, nbytes, fill=None):
+        if self.kind == "pageable":
+            a = np.empty(nbytes, np.uint8)
+        elif self.kind == "registered":
+            a = np.empty(nbytes + 4096, np.uint8)
+            off = (-a.ctypes.data) % 4096
+            a = a[off:off + nbytes]
+            r = self.ec.host_registered(a)
+            r.__enter__()
+            self.regs.append(r)
+        else:
+            extra = 8 if self.kind == "misaligned" else 0
+            p = self.ec.PinnedArray(nbytes + extra)
+            self.keep.append(p)
+            a = p.array[extra:]
+        if fill is not None:
+            a[:] = fill
+        return a
+
+    def close(self):
+        for r in self.regs:
+            r.__exit__()
+        for p in self.keep:
+            p.free()
+
+
+KINDS = ["pinned", "pageable", "misaligned", "registered", "mixed"]
+
+
+def _alloc(ec, kind, i):
+    """kind 'mixed' alternates pinned / pageable per buffer."""
+    if kind == "mixed":
+        return "pinned" if i % 2 == 0 else "pageable"
+    return kind
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("k,n", [(4, 6), (8, 12), (5, 7)])
+def test_encode_decode_host_kinds(ec, oracle, kind, k, n):
+    nst = 40000 if k <= 5 else 20000       # 2-3 staged batches, ragged tail
+    data = rand_bytes(CHUNK * k * nst, seed=k * 7 + n)
+    want = oracle.encode(k, n, data, nthreads=8)
+    pools = {t: Bufs(ec, t) for t in ("pinned", "pageable", "misaligned", "registered")}
+    try:
+        src = pools[_alloc(ec, kind, 0)].new(data.size, data)
+        frags = [pools[_alloc(ec, kind, i + 1)].new(CHUNK * nst, 0xA5) for i in range(n)]
+        rows = sorted(int(r) + 1 for r in np.random.default_rng(k).choice(n, k, replace=False))
+        mask = sum(1 << (r - 1) for r in rows)
+        out = pools[_alloc(ec, kind, 1)].new(data.size, 0)
+        with ec.ECMatrixList(k, n) as L:
+            L.encode_batch(nst, src, frags)
+            for i in range(n):
+                assert np.array_equal(frags[i], want[i]), "fragment %d" % i
+            L.decode_batch(nst, mask, rows, [frags[r - 1] for r in rows], out)
+        assert np.array_equal(out, data)
+    finally:
+        for p in pools.values():
+            p.close()
+
+
+def test_in_place_multi_batch(ec, oracle):
+    """All-pinned 4+2 over more than one in-place batch (256 MiB input)."""
+    k, n = 4, 6
+    nst = (300 << 20) // (CHUNK * k)
+    pool = Bufs(ec, "pinned")
+    try:
+        src = pool.new(CHUNK * k * nst)
+        src[:] = rand_bytes(src.size, seed=5)
+        frags = [pool.new(CHUNK * nst) for _ in range(n)]
+        out = pool.new(src.size, 0)
+        with ec.ECMatrixList(k, n) as L:
+            L.encode_batch(nst, src, frags)
+            want = oracle.encode(k, n, src[:CHUNK * k * 4096], nthreads=8)
+            for i in range(n):                   # prefix vs oracle ...
+                assert np.array_equal(frags[i][:CHUNK * 4096], want[i])
+            rows = [3, 4, 5, 6]                  # ... whole range by round trip
+            L.decode_batch(nst, 0x3C, rows, [frags[r - 1] for r in rows], out)
+        assert np.array_equal(out, src)
+    finally:
+        pool.close()
+
+
+@pytest.mark.parametrize("kind", ["pinned", "pageable", "mixed"])
+def test_decode_mixed_and_heal_host_kinds(ec, oracle, kind):
+    k, n, group = 4, 6, 64
+    nst = 100000 - 17                          # several batches, ragged last group
+    data = rand_bytes(CHUNK * k * nst, seed=9)
+    enc = oracle.encode(k, n, data, nthreads=8)
+    pools = {t: Bufs(ec, t) for t in ("pinned", "pageable")}
+    try:
+        frags = [pools[_alloc(ec, kind, i)].new(CHUNK * nst, enc[i]) for i in range(n)]
+        out = pools[_alloc(ec, kind, 1)].new(data.size, 0)
+        ngroups = (nst + group - 1) // group
+        rng = np.random.default_rng(2)
+        pool_masks = [0x3C, 0x0F, 0x33, 0x2B]
+        masks = [pool_masks[i] for i in rng.integers(0, len(pool_masks), ngroups)]
+        with ec.ECMatrixList(k, n) as L:
+            L.decode_mixed(nst, group, masks, frags, out)
+            assert np.array_equal(out, data)
+            outs = [pools[_alloc(ec, kind, i)].new(CHUNK * nst, 0) for i in range(2)]
+            rows = [3, 4, 5, 6]
+            L.heal(nst, 0x3C, [frags[r - 1] for r in rows], 0x03, outs)
+            assert np.array_equal(outs[0], enc[0]) and np.array_equal(outs[1], enc[1])
+    finally:
+        for p in pools.values():
+            p.close()
+
+
+def test_register_errors(ec):
+    import ctypes
+    lib = ec.ec_method.lib
+    a = np.empty(1 << 20, np.uint8)
+    assert lib.ec_method_host_register(None, 4096) == -22
+    assert lib.ec_method_host_register(ctypes.c_void_p(a.ctypes.data), 0) == -22
+    assert lib.ec_method_host_unregister(ctypes.c_void_p(a.ctypes.data)) == -22
+    with ec.host_registered(a):
+        pass
