@@ -8,8 +8,9 @@
 #include "ec_device.h"
 
 int ecdk_has_vander(uint32_t k, uint32_t n);
+/* zc: buffers are pinned host memory coded over PCIe (ec_encode_vander_zc) */
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
-                       const void *in, void *const *out);
+                       const void *in, void *const *out, bool zc = false);
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d);
 
 namespace ecdev {

@@ -28,11 +28,16 @@ using namespace ecdev;
 namespace {
 
 template <int K, int N, int W, bool NTS = false>
-int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
+int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const *out, bool zc)
 {
     FragPtrs f;
     for (int i = 0; i < N; ++i)
         f.p[i] = static_cast<uint8_t *>(out[i]);
+    if (zc && vander_use_zc<W>(nstripes)) {
+        hipLaunchKernelGGL((ec_encode_vander_zc<K, N, W>), dim3((u32)kZcBlocks), dim3(kBlock), 0,
+                           s, static_cast<const uint8_t *>(in), f, nstripes);
+        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    }
     const uint64_t g = vander_grid<W>(nstripes);
     if (g == 0)
         return 0;
@@ -44,15 +49,18 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
 }
 
 template <int K, int TS, int NW>
-int launch_combine(hipStream_t s, const CombineArgs &a)
+int launch_combine(hipStream_t s, const CombineArgs &a, uint64_t ntiles)
 {
-    const uint64_t g = combine_grid<TS>(a.nstripes);
+    const uint64_t g = a.tiles ? ntiles : combine_grid<TS>(a.nstripes);
     if (g == 0)
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
     const size_t lds = combine_lds<TS>(a.k);
-    if (a.group_pattern)
+    if (a.tiles)
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, false, true, false, true>),
+                           dim3((u32)g), dim3(NW * 64), lds, s, a);
+    else if (a.group_pattern)
         hipLaunchKernelGGL((ec_combine<K, TS, NW, true, false, true>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
     else
@@ -70,16 +78,16 @@ int ecdk_has_vander(uint32_t k, uint32_t n)
 }
 
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
-                       const void *in, void *const *out)
+                       const void *in, void *const *out, bool zc)
 {
     if (k == 2 && n == 3)
-        return launch_vander<2, 3, 4>(s, nstripes, in, out);
+        return launch_vander<2, 3, 4>(s, nstripes, in, out, zc);
     if (k == 4 && n == 6)
-        return launch_vander<4, 6, 2>(s, nstripes, in, out);
+        return launch_vander<4, 6, 2>(s, nstripes, in, out, zc);
     if (k == 8 && n == 12)
-        return launch_vander<8, 12, 1>(s, nstripes, in, out);
+        return launch_vander<8, 12, 1>(s, nstripes, in, out, zc);
     if (k == 16 && n == 20)
-        return launch_vander<16, 20, 1, true>(s, nstripes, in, out);
+        return launch_vander<16, 20, 1, true>(s, nstripes, in, out, zc);
     return -ENOTSUP;
 }
 
@@ -99,6 +107,10 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
     a->out_stride = d->out_stride;
     a->nstripes = d->nstripes;
     a->group_pattern = d->group_pattern;
+    a->tiles = d->tiles;
+    a->tile_bytes = d->tile_bytes;
+    if (d->tiles && (d->group_pattern || d->tile_bytes < ecd_seg_tile_bytes(d->k, d->rows)))
+        return -EINVAL;
     a->k = d->k;
     a->kw = (d->k + 3) / 4;
     a->rows = d->rows;
@@ -124,12 +136,23 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
     int rc = ecdk_pack_args(d, &a);
     if (rc)
         return rc;
+    const uint64_t nt = d->ntiles;
     /* a 16-stripe tile must not straddle two pattern groups */
     if (d->k <= 4 && (!d->group_pattern || d->group_shift >= 4))
-        return launch_combine<4, 2, 4>(s, a);
+        return launch_combine<4, 2, 4>(s, a, nt);
     if (d->k <= 4)
-        return launch_combine<4, 1, 4>(s, a);
+        return launch_combine<4, 1, 4>(s, a, nt);
     if (d->k <= 8)
-        return launch_combine<8, 1, 8>(s, a);
-    return launch_combine<16, 1, 8>(s, a);
+        return launch_combine<8, 1, 8>(s, a, nt);
+    return launch_combine<16, 1, 8>(s, a, nt);
+}
+
+uint32_t ecd_seg_tile_stripes(uint32_t k)
+{
+    return k <= 4 ? 16 : 8; /* the tile of the launch ecdk_combine picks */
+}
+
+uint32_t ecd_seg_tile_bytes(uint32_t k, uint32_t rows)
+{
+    return (uint32_t)((sizeof(ecd_seg_tile_t) + (k + rows) * sizeof(void *) + 15) & ~15ul);
 }

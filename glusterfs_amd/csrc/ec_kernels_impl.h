@@ -198,6 +198,69 @@ inline uint64_t vander_grid(uint64_t nstripes)
     return (nstripes * (16 / W) + kBlock - 1) / kBlock;
 }
 
+/* Zero-copy variant for buffers in pinned host memory, read and written by
+ * the CUs over PCIe.  In ec_encode_vander every resident wave loads, then
+ * stores, so a grid that fits the chip at once (any call below ~64 MiB)
+ * uses the link in one direction at a time: a 4 MiB 4+2 call took 189 us =
+ * 4 MiB in at ~56 GB/s, then 6 MiB out at ~55 GB/s (profiles/smallcalls_r01).
+ * Here a smaller grid strides over the stripes and each thread prefetches
+ * its next stripe before it computes and stores the current one, so the
+ * reads of one stripe overlap the writes of the previous one and the link
+ * runs both directions at once (~45 GB/s each way, tools/kbench/zerocopy). */
+template <int K, int N, int W, int BS = kBlock>
+__global__ __launch_bounds__(BS) void ec_encode_vander_zc(const uint8_t *__restrict__ in,
+                                                          const FragPtrs out, uint64_t nstripes)
+{
+    constexpr int L = 16 / W;
+    const uint64_t gtid = (uint64_t)blockIdx.x * BS + threadIdx.x;
+    const uint64_t step = (uint64_t)gridDim.x * (BS / L);
+    const u32 colb = (u32)(gtid % L) * (4 * W);
+    uint64_t stripe = gtid / L;
+    if (stripe >= nstripes)
+        return;
+
+    u32 x[K][8][W];
+    const uint8_t *s = in + stripe * (uint64_t)(K * ECD_CHUNK) + colb;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        load_chunk<W>(s + j * ECD_CHUNK, x[j]);
+    for (;;) {
+        const uint64_t nxt = stripe + step;
+        u32 y[K][8][W];
+        if (nxt < nstripes) {
+            const uint8_t *sn = in + nxt * (uint64_t)(K * ECD_CHUNK) + colb;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                load_chunk<W>(sn + j * ECD_CHUNK, y[j]);
+        }
+        encode_rows<K, W, false>(std::make_integer_sequence<int, N>{}, x, out,
+                                 stripe * (uint64_t)ECD_CHUNK + colb);
+        if (nxt >= nstripes)
+            break;
+        stripe = nxt;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    x[j][b][w] = y[j][b][w];
+    }
+}
+
+/* Zero-copy grid (tools/kbench/zcenc, profiles/zcenc_r01.log): 32 blocks
+ * keep far more bytes in flight than the link's bandwidth-delay product;
+ * 16 MiB / 64 MiB 4+2 calls ran 619 / 2206 us against 730 / 2446 us one-pass
+ * (+11-18 %).  At <= 4 MiB the prefetch cannot desynchronise enough waves
+ * and the one-pass kernel is as fast or faster, so it is used there. */
+constexpr uint64_t kZcBlocks = 32;
+
+template <int W>
+inline bool vander_use_zc(uint64_t nstripes)
+{
+    return nstripes * (16 / W) > 4 * kZcBlocks * kBlock;
+}
+
 /* ------------------------------------------------- generic combination */
 
 constexpr int kPatWords = 512; /* kernel-argument pattern space (2 KiB) */
@@ -212,7 +275,8 @@ struct CombineArgs {
     uint8_t *out_base[ECD_MAX_ROWS];
     uint64_t in_stride, out_stride, nstripes;
     const uint8_t *group_pattern;
-    u32 k, kw, rows, group_shift, pwords;
+    const uint8_t *tiles; /* SEG: ecd_seg_tile_t table, tile_bytes apart */
+    u32 k, kw, rows, group_shift, pwords, tile_bytes;
     u32 pat[kPatWords];
 };
 
@@ -235,8 +299,12 @@ __device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
 /* K: max inputs (k <= K); TS: tile = 8*TS stripes; NW: waves per block;
  * GLDS: stage the tile with LDS-DMA (global_load_lds_dwordx4, no VGPRs)
  * instead of global_load + ds_write; PF: issue the next input's LDS reads
- * before each multiply. */
-template <int K, int TS, int NW, bool MIXED, bool NTS, bool GLDS = false, bool PF = false>
+ * before each multiply; SEG: block b codes the tile described by
+ * ecd_seg_tile_t b of a.tiles -- its own input/output pointers, stripe count
+ * and pattern -- so one launch serves many independent small calls (the
+ * coalescing queue of ec_device.hip). */
+template <int K, int TS, int NW, bool MIXED, bool NTS, bool GLDS = false, bool PF = false,
+          bool SEG = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -246,13 +314,34 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
     const u32 k = a.k;
-    const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
 
+    uint64_t t0 = (uint64_t)blockIdx.x * T, nst = a.nstripes;
     u32 pb = 0;
+    const ecd_seg_tile_t *tile = nullptr;
+    if constexpr (SEG) {
+        tile = reinterpret_cast<const ecd_seg_tile_t *>(a.tiles +
+                                                        (uint64_t)blockIdx.x * a.tile_bytes);
+        t0 = 0;
+        nst = tile->nstripes;
+        pb = tile->pattern * a.pwords;
+    }
     if constexpr (MIXED)
         pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
+    /* base address of input slot `src` / output row `r` */
+    auto inb = [&](u32 src) -> const uint8_t * {
+        if constexpr (SEG)
+            return tile->ptr[src];
+        else
+            return a.in_base[src];
+    };
+    auto outb = [&](u32 r) -> uint8_t * {
+        if constexpr (SEG)
+            return const_cast<uint8_t *>(tile->ptr[k + r]);
+        else
+            return a.out_base[r];
+    };
 
     if constexpr (GLDS) {
         /* every wave instruction fills 1 KiB of LDS linearly (2 chunks of one
@@ -270,9 +359,9 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             const u32 e = ins * 64 + lane;            /* LDS piece */
             const u32 s = (e / 32) % T, slot = e & 31u;
             const uint64_t st = t0 + s;
-            if (st < a.nstripes) {
+            if (st < nst) {
                 const u32 src = pat_byte(a, pb, p);
-                const uint8_t *g = a.in_base[src] + st * a.in_stride +
+                const uint8_t *g = inb(src) + st * a.in_stride +
                                    ((((slot >> 2) ^ (s & 3u)) << 6) | ((slot & 3u) << 4));
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void *)g,
@@ -288,9 +377,9 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             const u32 p = e / (T * 32), s = (e / 32) % T, q = e & 31u;
             const uint64_t st = t0 + s;
             v[j] = make_uint4(0, 0, 0, 0);
-            if (p < k && st < a.nstripes) {
+            if (p < k && st < nst) {
                 const u32 src = pat_byte(a, pb, p);
-                v[j] = *reinterpret_cast<const uint4 *>(a.in_base[src] + st * a.in_stride +
+                v[j] = *reinterpret_cast<const uint4 *>(inb(src) + st * a.in_stride +
                                                         q * 16u);
             }
         }
@@ -355,8 +444,8 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             }
         }
         const uint64_t ost = t0 + s;
-        if (ost < a.nstripes)
-            store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+        if (ost < nst)
+            store_chunk<CW, NTS>(outb(r) + ost * a.out_stride + cc * 8u, acc);
     }
 }
 
