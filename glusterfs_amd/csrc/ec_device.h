@@ -37,28 +37,9 @@ typedef struct ecd_combine_desc {
     uint32_t group_shift;         /* log2(stripes per pattern group), >= 3   */
     uint32_t npatterns;
     uint32_t pat_bytes;           /* bytes per packed pattern = k + rows*k   */
-    /* Segmented launch (tiles != NULL): block b codes tile b, an
-     * ecd_seg_tile_t at tiles + b*tile_bytes in device-visible memory, with
-     * its own pointers, stripe count (<= ecd_seg_tile_stripes(k)) and
-     * pattern; in_base / out_base / nstripes / group_pattern are unused. */
-    uint32_t tile_bytes;
-    const uint8_t *tiles;
-    uint64_t ntiles;
+    uint32_t pad;
     uint8_t pat[ECD_MAX_PAT_BYTES];
 } ecd_combine_desc_t;
-
-/* One tile of a segmented combine launch: ptr[0..k) are the inputs
- * (pattern p reads ptr[src[p]]), ptr[k..k+rows) the output rows, each
- * already offset to the tile's first stripe. */
-typedef struct ecd_seg_tile {
-    uint32_t nstripes;
-    uint32_t pattern;
-    const uint8_t *ptr[];
-} ecd_seg_tile_t;
-
-/* Stripes per tile of a segmented launch and bytes per ecd_seg_tile_t. */
-uint32_t ecd_seg_tile_stripes(uint32_t k);
-uint32_t ecd_seg_tile_bytes(uint32_t k, uint32_t rows);
 
 /* Number of usable gfx950 devices (0 when none: callers fail, there is no
  * CPU fallback anywhere in the product path). */

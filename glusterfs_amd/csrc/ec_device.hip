@@ -551,332 +551,63 @@ int run_decode_dev(int dev, const DecodeJob &j)
     return rc;
 }
 
-/* ------------------------------------------------ small-call coalescing */
+/* ------------------------------------------------ device placement */
 
-/* GlusterFS codes one fop at a time on many client threads: 128 KiB
- * FUSE / write-behind writes (fuse-bridge.c:5179, write-behind.c:3198) up to
- * 4 MiB self-heal blocks, each a separate ec_method_encode / _decode call
- * (SURVEY.md 8f rank 2).  One launch per call pays a launch, a stream
- * synchronisation and a sub-chip grid every time, and splitting such a call
- * across 8 GPUs multiplies that.  So calls up to queue_max_bytes() go to ONE
- * device (the one with the fewest bytes in flight) and through a per-device
- * group-commit queue: a caller that finds a free lane becomes the leader,
- * takes every queued request of its shape (k, rows, strides) and codes them
- * all in one segmented ec_combine launch (one tile descriptor per block,
- * ecd_seg_tile_t, read by the kernel from pinned host memory); callers that
- * arrive meanwhile queue behind it and ride the next launch.  An uncontended
- * call leads its own one-request batch, so it pays no extra thread hop. */
-uint64_t queue_max_bytes()
+/* GlusterFS codes one fop per call on many client threads: 128 KiB
+ * FUSE / write-behind writes (fuse-bridge.c:5179, write-behind.c:3198) up
+ * to 4 MiB self-heal blocks.  Splitting such a call
+ * across all GPUs of the node multiplies its fixed cost (a launch and a
+ * synchronisation per device, ~20 us) for PCIe time it does not save, so a
+ * call below split_min_bytes() runs whole on the device with the fewest
+ * bytes in flight; concurrent calls spread over the devices and overlap on
+ * per-call streams.  (Coalescing concurrent calls into one segmented launch
+ * was measured slower on MI355X -- see DESIGN.md, profiles/smallcalls_r01_*.) */
+uint64_t split_min_bytes()
 {
     static const uint64_t v = [] {
-        const char *e = getenv("EC_QUEUE_MAX_MB");
-        const long mb = e ? atol(e) : 8;
-        return (uint64_t)(mb >= 0 && mb <= 1024 ? mb : 8) << 20;
+        const char *e = getenv("EC_SPLIT_MIN_MB");
+        const long mb = e ? atol(e) : 64;
+        return (uint64_t)(mb >= 0 && mb <= 65536 ? mb : 64) << 20;
     }();
     return v;
 }
 
-constexpr int kLanes = 2;                    /* concurrent batches per device */
-constexpr uint64_t kBatchBytes = 64ull << 20; /* coalesce up to this much     */
+std::atomic<uint64_t> g_inflight[kMaxDev];
 
-struct SegReq {
-    uint32_t k, rows;
-    uint64_t in_stride, out_stride, nstripes;
-    const uint8_t *in[ECD_MAX_K];            /* kernel-visible, pattern order */
-    uint8_t *out[ECD_MAX_ROWS];
-    uint8_t pat[ECD_MAX_K + ECD_MAX_ROWS * ECD_MAX_K]; /* identity src + coef */
-    uint32_t pat_bytes;
-    bool done = false;
-    int rc = 0;
-
-    uint64_t bytes() const { return nstripes * ECD_CHUNK * (k + rows); }
-    bool same_shape(const SegReq &o) const
-    {
-        return k == o.k && rows == o.rows && in_stride == o.in_stride &&
-               out_stride == o.out_stride;
-    }
-};
-
-struct Lane {
-    hipStream_t stream = nullptr;
-    uint8_t *tiles = nullptr; /* pinned tile descriptors */
-    size_t cap = 0;
-};
-
-struct DevQueue {
-    std::mutex mu;
-    std::condition_variable cv;
-    std::deque<SegReq *> q;
-    std::vector<Lane *> idle;
-    int nlanes = 0;
-    std::atomic<uint64_t> inflight{0};
-};
-
-DevQueue g_q[kMaxDev];
-
-Lane *make_lane(int dev)
-{
-    Lane *L = new Lane;
-    if (hipSetDevice(g_dev_ids[dev]) != hipSuccess ||
-        hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess) {
-        (void)hipGetLastError();
-        delete L;
-        return nullptr;
-    }
-    return L;
-}
-
-/* Take the oldest queued request and every later one of the same shape
- * while the batch's patterns fit the kernel-argument table. */
-std::vector<SegReq *> take_batch(DevQueue &Q)
-{
-    std::vector<SegReq *> b;
-    if (Q.q.empty())
-        return b;
-    const SegReq &h = *Q.q.front();
-    const uint32_t kw = (h.k + 3) / 4;
-    const uint32_t max_pat = std::min<uint32_t>(512 / (kw * (1 + h.rows)),
-                                                ECD_MAX_PAT_BYTES / h.pat_bytes);
-    std::vector<const uint8_t *> pats;
-    uint64_t bytes = 0;
-    for (auto it = Q.q.begin(); it != Q.q.end();) {
-        SegReq *r = *it;
-        if (!r->same_shape(h) || (bytes && bytes + r->bytes() > kBatchBytes)) {
-            ++it;
-            continue;
-        }
-        bool have = false;
-        for (const uint8_t *p : pats)
-            have |= memcmp(p, r->pat, r->pat_bytes) == 0;
-        if (!have && pats.size() == max_pat) {
-            ++it;
-            continue;
-        }
-        if (!have)
-            pats.push_back(r->pat);
-        bytes += r->bytes();
-        b.push_back(r);
-        it = Q.q.erase(it);
-    }
-    return b;
-}
-
-int run_seg_batch(int dev, Lane *L, const std::vector<SegReq *> &b)
-{
-    HIPCHK(hipSetDevice(g_dev_ids[dev]));
-    const SegReq &h = *b[0];
-    const uint32_t T = ecd_seg_tile_stripes(h.k), tb = ecd_seg_tile_bytes(h.k, h.rows);
-    uint64_t ntiles = 0;
-    for (const SegReq *r : b)
-        ntiles += (r->nstripes + T - 1) / T;
-    if (ntiles * tb > L->cap) {
-        if (L->tiles)
-            (void)hipHostFree(L->tiles);
-        L->tiles = nullptr;
-        L->cap = 0;
-        const size_t want = std::max<size_t>(ntiles * tb, 64 << 10);
-        HIPCHK(hipHostMalloc(&L->tiles, want, hipHostMallocDefault));
-        L->cap = want;
-    }
-    auto d = std::make_unique<ecd_combine_desc_t>();
-    memset(d.get(), 0, offsetof(ecd_combine_desc_t, pat));
-    d->k = h.k;
-    d->rows = h.rows;
-    d->in_stride = h.in_stride;
-    d->out_stride = h.out_stride;
-    d->pat_bytes = h.pat_bytes;
-    d->tiles = L->tiles;
-    d->tile_bytes = tb;
-    d->ntiles = ntiles;
-    uint64_t t = 0;
-    for (const SegReq *r : b) {
-        uint32_t pid = 0;
-        while (pid < d->npatterns &&
-               memcmp(d->pat + (size_t)pid * h.pat_bytes, r->pat, h.pat_bytes) != 0)
-            ++pid;
-        if (pid == d->npatterns)
-            memcpy(d->pat + (size_t)d->npatterns++ * h.pat_bytes, r->pat, h.pat_bytes);
-        for (uint64_t s0 = 0; s0 < r->nstripes; s0 += T, ++t) {
-            auto *tile = reinterpret_cast<ecd_seg_tile_t *>(L->tiles + t * tb);
-            tile->nstripes = (uint32_t)std::min<uint64_t>(T, r->nstripes - s0);
-            tile->pattern = pid;
-            for (uint32_t p = 0; p < h.k; ++p)
-                tile->ptr[p] = r->in[p] + s0 * h.in_stride;
-            for (uint32_t o = 0; o < h.rows; ++o)
-                tile->ptr[h.k + o] = r->out[o] + s0 * h.out_stride;
-        }
-    }
-    int rc = ecdk_combine(L->stream, d.get());
-    if (rc == 0)
-        HIPCHK(hipStreamSynchronize(L->stream));
-    return rc;
-}
-
-/* Queue `r` on device `dev` and return when it has been coded. */
-int seg_submit(int dev, SegReq *r)
-{
-    DevQueue &Q = g_q[dev];
-    std::unique_lock<std::mutex> g(Q.mu);
-    Q.q.push_back(r);
-    while (!r->done) {
-        Lane *L = nullptr;
-        if (!Q.idle.empty()) {
-            L = Q.idle.back();
-            Q.idle.pop_back();
-        } else if (Q.nlanes < kLanes) {
-            ++Q.nlanes;
-            g.unlock();
-            L = make_lane(dev);
-            g.lock();
-            if (!L) {
-                --Q.nlanes;
-                if (r->done)
-                    break;
-                for (auto it = Q.q.begin(); it != Q.q.end(); ++it)
-                    if (*it == r) {
-                        Q.q.erase(it);
-                        break;
-                    }
-                set_err("coalescing queue", hipErrorOutOfMemory);
-                return -EIO;
-            }
-        }
-        if (!L) {
-            Q.cv.wait(g);
-            continue;
-        }
-        std::vector<SegReq *> b = take_batch(Q);
-        if (b.empty()) {
-            /* r rides a batch another leader is running: wait for it */
-            Q.idle.push_back(L);
-            Q.cv.wait(g);
-            continue;
-        }
-        g.unlock();
-        const int rc = run_seg_batch(dev, L, b);
-        g.lock();
-        for (SegReq *x : b) {
-            x->rc = rc;
-            x->done = true;
-        }
-        Q.idle.push_back(L);
-        Q.cv.notify_all();
-    }
-    return r->rc;
-}
-
-/* Device for a small call: fewest bytes in flight, rotating on ties. */
+/* Device for a whole call: fewest bytes in flight, rotating on ties. */
 int pick_device(uint64_t bytes)
 {
     static std::atomic<unsigned> rr{0};
     const unsigned start = rr.fetch_add(1);
     int best = (int)(start % g_ndev);
-    uint64_t lo = g_q[best].inflight.load();
+    uint64_t lo = g_inflight[best].load();
     for (int i = 1; i < g_ndev; ++i) {
         const int d = (int)((start + i) % g_ndev);
-        const uint64_t v = g_q[d].inflight.load();
+        const uint64_t v = g_inflight[d].load();
         if (v < lo) {
             lo = v;
             best = d;
         }
     }
-    g_q[best].inflight.fetch_add(bytes);
+    g_inflight[best].fetch_add(bytes);
     return best;
-}
-
-/* One small host-buffer call.  req.in[] / req.out[] hold addresses inside
- * the caller's buffers `ins` / `outs`; buffers that are not pinned and
- * mapped are staged through a pinned Stage (the pointers are rebased onto
- * it), the request is queued, and staged outputs are copied back. */
-struct HostBuf {
-    uint8_t *p;
-    size_t n;
-};
-
-int small_call(SegReq &req, const std::vector<HostBuf> &ins, const std::vector<HostBuf> &outs)
-{
-    const uint64_t bytes = req.bytes();
-    const int dev = pick_device(bytes);
-    struct Done {
-        int dev;
-        uint64_t bytes;
-        ~Done() { g_q[dev].inflight.fetch_sub(bytes); }
-    } done{dev, bytes};
-    HIPCHK(hipSetDevice(g_dev_ids[dev]));
-    /* kernel-visible base of every buffer: itself when mapped, else a slice
-     * of the stage */
-    std::vector<uint8_t *> kin(ins.size()), kout(outs.size());
-    size_t need_in = 0, need_out = 0;
-    for (size_t i = 0; i < ins.size(); ++i)
-        if (!(kin[i] = mapped(ins[i].p, ins[i].n)))
-            need_in += (ins[i].n + 255) & ~size_t(255);
-    for (size_t i = 0; i < outs.size(); ++i)
-        if (!(kout[i] = mapped(outs[i].p, outs[i].n)))
-            need_out += (outs[i].n + 255) & ~size_t(255);
-    Stage *s = nullptr;
-    if (need_in || need_out) {
-        if (!(s = acquire(dev)))
-            return -EIO;
-        int rc = grow(s->pin_in, s->cap_in, need_in);
-        if (rc == 0)
-            rc = grow(s->pin_out, s->cap_out, need_out);
-        if (rc) {
-            release(s);
-            return rc;
-        }
-    }
-    std::vector<CopyPool::Piece> pc;
-    size_t off = 0;
-    for (size_t i = 0; i < ins.size(); ++i)
-        if (!kin[i]) {
-            kin[i] = s->pin_in[0] + off;
-            off += (ins[i].n + 255) & ~size_t(255);
-            add_copy(pc, kin[i], ins[i].p, ins[i].n);
-        }
-    off = 0;
-    for (size_t i = 0; i < outs.size(); ++i)
-        if (!kout[i]) {
-            kout[i] = s->pin_out[0] + off;
-            off += (outs[i].n + 255) & ~size_t(255);
-        }
-    g_copy_pool.run(pc);
-    auto rebase = [](const uint8_t *a, const std::vector<HostBuf> &bufs,
-                     const std::vector<uint8_t *> &k) -> uint8_t * {
-        for (size_t i = 0; i < bufs.size(); ++i)
-            if (a >= bufs[i].p && a < bufs[i].p + bufs[i].n)
-                return k[i] + (a - bufs[i].p);
-        return nullptr;
-    };
-    int rc = 0;
-    for (uint32_t p = 0; p < req.k && rc == 0; ++p)
-        if (!(req.in[p] = rebase(req.in[p], ins, kin)))
-            rc = -EINVAL;
-    for (uint32_t o = 0; o < req.rows && rc == 0; ++o)
-        if (!(req.out[o] = rebase(req.out[o], outs, kout)))
-            rc = -EINVAL;
-    if (rc == 0)
-        rc = seg_submit(dev, &req);
-    if (rc == 0 && need_out) {
-        pc.clear();
-        for (size_t i = 0; i < outs.size(); ++i)
-            if (kout[i] != outs[i].p)
-                add_copy(pc, outs[i].p, kout[i], outs[i].n);
-        g_copy_pool.run(pc);
-    }
-    if (s)
-        release(s);
-    return rc;
 }
 
 /* Run fn(dev, s0, s1) over a stripe-range partition; `align` keeps every
  * range boundary a multiple of it (pattern groups). */
 template <typename F>
-int partition(int ndev, uint64_t nstripes, uint64_t align, F fn)
+int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
 {
     if (g_ndev == 0)
         return -ENODEV;
     if (ndev <= 0 || ndev > g_ndev)
         ndev = g_ndev;
+    if (ndev > 1 && bytes < split_min_bytes()) {
+        const int d = pick_device(bytes);
+        const int rc = fn(d, 0, nstripes);
+        g_inflight[d].fetch_sub(bytes);
+        return rc;
+    }
     const uint64_t units = (nstripes + align - 1) / align;
     if ((uint64_t)ndev > units)
         ndev = (int)std::max<uint64_t>(1, units);
@@ -952,33 +683,14 @@ int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const v
 {
     if (ecd_device_count() == 0)
         return -ENODEV;
-    const uint64_t S = nstripes * k * ECD_CHUNK;
-    if (S <= queue_max_bytes() && k <= ECD_MAX_K && n <= ECD_MAX_ROWS) {
-        SegReq r;
-        r.k = k;
-        r.rows = n;
-        r.in_stride = (uint64_t)k * ECD_CHUNK;
-        r.out_stride = ECD_CHUNK;
-        r.nstripes = nstripes;
-        r.pat_bytes = k + n * k;
-        memcpy(r.pat, enc_pat, r.pat_bytes); /* src = 0..k-1: chunk p of a stripe */
-        uint8_t *inb = const_cast<uint8_t *>(static_cast<const uint8_t *>(in));
-        std::vector<HostBuf> ins{{inb, S}}, outs;
-        for (uint32_t p = 0; p < k; ++p)
-            r.in[p] = inb + (size_t)p * ECD_CHUNK;
-        for (uint32_t i = 0; i < n; ++i) {
-            r.out[i] = static_cast<uint8_t *>(out[i]);
-            outs.push_back({r.out[i], nstripes * ECD_CHUNK});
-        }
-        return small_call(r, ins, outs);
-    }
     EncodeJob base;
     base.k = k;
     base.n = n;
     base.in = static_cast<const uint8_t *>(in);
     base.out = reinterpret_cast<uint8_t *const *>(out);
     base.enc_pat = enc_pat;
-    return partition(ndev, nstripes, 1, [&](int d, uint64_t s0, uint64_t s1) {
+    return partition(ndev, nstripes, 1, nstripes * ECD_CHUNK * (k + n),
+                     [&](int d, uint64_t s0, uint64_t s1) {
         EncodeJob j = base;
         j.s0 = s0;
         j.s1 = s1;
@@ -987,7 +699,7 @@ int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const v
 }
 
 int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, uint32_t nfrags,
-                    const void *const *frags, void *out, void *const *outs_, uint32_t npatterns,
+                    const void *const *frags, void *out, void *const *outs, uint32_t npatterns,
                     const uint8_t *pats, const uint8_t *group_pattern, uint32_t group_shift)
 {
     if (ecd_device_count() == 0)
@@ -998,39 +710,6 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, uint
         return -EINVAL;
     if (group_pattern && (group_shift < 3 || group_shift > 40))
         return -EINVAL;
-    const uint64_t F = nstripes * ECD_CHUNK;
-    if (npatterns == 1 && !group_pattern && F * k <= queue_max_bytes()) {
-        SegReq r;
-        r.k = k;
-        r.rows = rows;
-        r.in_stride = ECD_CHUNK;
-        r.nstripes = nstripes;
-        r.pat_bytes = k + rows * k;
-        memcpy(r.pat, pats, r.pat_bytes);
-        std::vector<HostBuf> ins, outs;
-        for (uint32_t p = 0; p < k; ++p) {
-            const uint32_t f = pats[p];
-            if (f >= nfrags || !frags[f])
-                return -EINVAL;
-            r.pat[p] = (uint8_t)p; /* the tile lists the k inputs in order */
-            r.in[p] = static_cast<const uint8_t *>(frags[f]);
-            ins.push_back({const_cast<uint8_t *>(r.in[p]), F});
-        }
-        if (outs_) {
-            r.out_stride = ECD_CHUNK;
-            for (uint32_t o = 0; o < rows; ++o) {
-                r.out[o] = static_cast<uint8_t *>(outs_[o]);
-                outs.push_back({r.out[o], F});
-            }
-        } else {
-            r.out_stride = (uint64_t)rows * ECD_CHUNK;
-            uint8_t *ob = static_cast<uint8_t *>(out);
-            for (uint32_t o = 0; o < rows; ++o)
-                r.out[o] = ob + (size_t)o * ECD_CHUNK;
-            outs.push_back({ob, F * rows});
-        }
-        return small_call(r, ins, outs);
-    }
     DecodeJob base;
     base.k = k;
     base.rows = rows;
@@ -1039,11 +718,12 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, uint
     base.group_shift = group_shift;
     base.frags = reinterpret_cast<const uint8_t *const *>(frags);
     base.out = static_cast<uint8_t *>(out);
-    base.outs = reinterpret_cast<uint8_t *const *>(outs_);
+    base.outs = reinterpret_cast<uint8_t *const *>(outs);
     base.pats = pats;
     base.group_pattern = group_pattern;
     const uint64_t align = group_pattern ? (1ull << group_shift) : 1;
-    return partition(ndev, nstripes, align, [&](int d, uint64_t s0, uint64_t s1) {
+    return partition(ndev, nstripes, align, nstripes * ECD_CHUNK * (nfrags + rows),
+                     [&](int d, uint64_t s0, uint64_t s1) {
         DecodeJob j = base;
         j.s0 = s0;
         j.s1 = s1;

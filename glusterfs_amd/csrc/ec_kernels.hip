@@ -49,18 +49,15 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
 }
 
 template <int K, int TS, int NW>
-int launch_combine(hipStream_t s, const CombineArgs &a, uint64_t ntiles)
+int launch_combine(hipStream_t s, const CombineArgs &a)
 {
-    const uint64_t g = a.tiles ? ntiles : combine_grid<TS>(a.nstripes);
+    const uint64_t g = combine_grid<TS>(a.nstripes);
     if (g == 0)
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
     const size_t lds = combine_lds<TS>(a.k);
-    if (a.tiles)
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, false, true, false, true>),
-                           dim3((u32)g), dim3(NW * 64), lds, s, a);
-    else if (a.group_pattern)
+    if (a.group_pattern)
         hipLaunchKernelGGL((ec_combine<K, TS, NW, true, false, true>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
     else
@@ -107,10 +104,6 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
     a->out_stride = d->out_stride;
     a->nstripes = d->nstripes;
     a->group_pattern = d->group_pattern;
-    a->tiles = d->tiles;
-    a->tile_bytes = d->tile_bytes;
-    if (d->tiles && (d->group_pattern || d->tile_bytes < ecd_seg_tile_bytes(d->k, d->rows)))
-        return -EINVAL;
     a->k = d->k;
     a->kw = (d->k + 3) / 4;
     a->rows = d->rows;
@@ -136,23 +129,12 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
     int rc = ecdk_pack_args(d, &a);
     if (rc)
         return rc;
-    const uint64_t nt = d->ntiles;
     /* a 16-stripe tile must not straddle two pattern groups */
     if (d->k <= 4 && (!d->group_pattern || d->group_shift >= 4))
-        return launch_combine<4, 2, 4>(s, a, nt);
+        return launch_combine<4, 2, 4>(s, a);
     if (d->k <= 4)
-        return launch_combine<4, 1, 4>(s, a, nt);
+        return launch_combine<4, 1, 4>(s, a);
     if (d->k <= 8)
-        return launch_combine<8, 1, 8>(s, a, nt);
-    return launch_combine<16, 1, 8>(s, a, nt);
-}
-
-uint32_t ecd_seg_tile_stripes(uint32_t k)
-{
-    return k <= 4 ? 16 : 8; /* the tile of the launch ecdk_combine picks */
-}
-
-uint32_t ecd_seg_tile_bytes(uint32_t k, uint32_t rows)
-{
-    return (uint32_t)((sizeof(ecd_seg_tile_t) + (k + rows) * sizeof(void *) + 15) & ~15ul);
+        return launch_combine<8, 1, 8>(s, a);
+    return launch_combine<16, 1, 8>(s, a);
 }

@@ -275,8 +275,7 @@ struct CombineArgs {
     uint8_t *out_base[ECD_MAX_ROWS];
     uint64_t in_stride, out_stride, nstripes;
     const uint8_t *group_pattern;
-    const uint8_t *tiles; /* SEG: ecd_seg_tile_t table, tile_bytes apart */
-    u32 k, kw, rows, group_shift, pwords, tile_bytes;
+    u32 k, kw, rows, group_shift, pwords;
     u32 pat[kPatWords];
 };
 
@@ -299,12 +298,8 @@ __device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
 /* K: max inputs (k <= K); TS: tile = 8*TS stripes; NW: waves per block;
  * GLDS: stage the tile with LDS-DMA (global_load_lds_dwordx4, no VGPRs)
  * instead of global_load + ds_write; PF: issue the next input's LDS reads
- * before each multiply; SEG: block b codes the tile described by
- * ecd_seg_tile_t b of a.tiles -- its own input/output pointers, stripe count
- * and pattern -- so one launch serves many independent small calls (the
- * coalescing queue of ec_device.hip). */
-template <int K, int TS, int NW, bool MIXED, bool NTS, bool GLDS = false, bool PF = false,
-          bool SEG = false>
+ * before each multiply. */
+template <int K, int TS, int NW, bool MIXED, bool NTS, bool GLDS = false, bool PF = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -314,34 +309,13 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
     const u32 k = a.k;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
 
-    uint64_t t0 = (uint64_t)blockIdx.x * T, nst = a.nstripes;
     u32 pb = 0;
-    const ecd_seg_tile_t *tile = nullptr;
-    if constexpr (SEG) {
-        tile = reinterpret_cast<const ecd_seg_tile_t *>(a.tiles +
-                                                        (uint64_t)blockIdx.x * a.tile_bytes);
-        t0 = 0;
-        nst = tile->nstripes;
-        pb = tile->pattern * a.pwords;
-    }
     if constexpr (MIXED)
         pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
-    /* base address of input slot `src` / output row `r` */
-    auto inb = [&](u32 src) -> const uint8_t * {
-        if constexpr (SEG)
-            return tile->ptr[src];
-        else
-            return a.in_base[src];
-    };
-    auto outb = [&](u32 r) -> uint8_t * {
-        if constexpr (SEG)
-            return const_cast<uint8_t *>(tile->ptr[k + r]);
-        else
-            return a.out_base[r];
-    };
 
     if constexpr (GLDS) {
         /* every wave instruction fills 1 KiB of LDS linearly (2 chunks of one
@@ -359,9 +333,9 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             const u32 e = ins * 64 + lane;            /* LDS piece */
             const u32 s = (e / 32) % T, slot = e & 31u;
             const uint64_t st = t0 + s;
-            if (st < nst) {
+            if (st < a.nstripes) {
                 const u32 src = pat_byte(a, pb, p);
-                const uint8_t *g = inb(src) + st * a.in_stride +
+                const uint8_t *g = a.in_base[src] + st * a.in_stride +
                                    ((((slot >> 2) ^ (s & 3u)) << 6) | ((slot & 3u) << 4));
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void *)g,
@@ -377,9 +351,9 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             const u32 p = e / (T * 32), s = (e / 32) % T, q = e & 31u;
             const uint64_t st = t0 + s;
             v[j] = make_uint4(0, 0, 0, 0);
-            if (p < k && st < nst) {
+            if (p < k && st < a.nstripes) {
                 const u32 src = pat_byte(a, pb, p);
-                v[j] = *reinterpret_cast<const uint4 *>(inb(src) + st * a.in_stride +
+                v[j] = *reinterpret_cast<const uint4 *>(a.in_base[src] + st * a.in_stride +
                                                         q * 16u);
             }
         }
@@ -444,8 +418,8 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             }
         }
         const uint64_t ost = t0 + s;
-        if (ost < nst)
-            store_chunk<CW, NTS>(outb(r) + ost * a.out_stride + cc * 8u, acc);
+        if (ost < a.nstripes)
+            store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
     }
 }
 

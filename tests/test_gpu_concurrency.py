@@ -1,13 +1,13 @@
-"""GPU parity of the small-call coalescing queue (ec_device.hip,
-"small-call coalescing").
+"""GPU parity of host-buffer calls made concurrently from many threads,
+the way GlusterFS client threads call the coder (SURVEY.md 8f rank 2:
+128 KiB FUSE / write-behind writes up to 4 MiB heal blocks, several volumes
+per client, each fop its own call).
 
-Host-buffer calls up to EC_QUEUE_MAX_MB (8 MiB of user data) from many
-threads are merged into segmented ec_combine launches: one tile descriptor
-per block, per-request pointers, deduplicated patterns.  These tests drive
-it the way GlusterFS client threads do (concurrent encode / decode / heal
-on several volumes with different geometries, masks and buffer kinds) and
-check every result bit-exactly against the CPU oracle.  ctypes releases
-the GIL, so the Python threads really call the library concurrently.
+Every call runs on its own stream; calls below EC_SPLIT_MIN_MB run whole on
+one device (ec_device.hip "device placement").  The tests mix geometries,
+masks, buffer kinds and the decode-matrix cache under contention and check
+every result bit-exactly against the CPU oracle.  ctypes releases the GIL,
+so the Python threads really call the library concurrently.
 """
 import threading
 
@@ -17,7 +17,6 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 CHUNK = 512
-QUEUE_MAX = 8 << 20
 
 
 @pytest.fixture(scope="module")
@@ -106,9 +105,9 @@ def test_concurrent_mixed_geometries(ec, oracle, kind):
             p.free()
 
 
-def test_many_masks_overflow_pattern_table(ec, oracle):
-    """More distinct 8+4 masks in flight than one launch's pattern table
-    holds (28 for 8+4 decode): the queue must split them over launches."""
+def test_many_masks_concurrent_cache(ec, oracle):
+    """48 distinct 8+4 masks from 16 threads: the decode-matrix cache
+    (ec-method.c:200-256 semantics, max=64) under contention."""
     k, n, nst = 8, 12, 40
     data = [rand_bytes(CHUNK * k * nst, seed=s) for s in range(4)]
     enc = [oracle.encode(k, n, d) for d in data]
@@ -127,24 +126,6 @@ def test_many_masks_overflow_pattern_table(ec, oracle):
                 L.decode_batch(nst, m, rows, [enc[d][r - 1] for r in rows], out)
                 assert np.array_equal(out, data[d]), (t, j, hex(m))
         run_threads(worker, 16)
-
-
-@pytest.mark.parametrize("extra", [0, 1])
-def test_queue_size_boundary(ec, oracle, extra):
-    """Exactly the queue limit goes through the queue; one stripe more
-    through the pipeline; both bit-exact."""
-    k, n = 4, 6
-    nst = QUEUE_MAX // (CHUNK * k) + extra
-    data = rand_bytes(CHUNK * k * nst, seed=31 + extra)
-    want = oracle.encode(k, n, data, nthreads=8)
-    frags = [np.zeros(CHUNK * nst, np.uint8) for _ in range(n)]
-    out = np.zeros_like(data)
-    with ec.ECMatrixList(k, n) as L:
-        L.encode_batch(nst, data, frags)
-        for i in range(n):
-            assert np.array_equal(frags[i], want[i])
-        L.decode_batch(nst, 0x33, [1, 2, 5, 6], [frags[0], frags[1], frags[4], frags[5]], out)
-    assert np.array_equal(out, data)
 
 
 def test_drop_in_encode_advances_pointers_under_concurrency(ec, oracle):
