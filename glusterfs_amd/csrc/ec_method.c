@@ -389,6 +389,84 @@ pack_pattern(uint8_t *dst, uint32_t k, const uint8_t *src, uint32_t rows,
     return k + rows * k;
 }
 
+/* --------------------------------------------------- on-disk config guard */
+
+#define ECM_CONFIG_VERSION 0   /* EC_CONFIG_VERSION, ec-common.h:22   */
+#define ECM_CONFIG_ALGORITHM 0 /* EC_CONFIG_ALGORITHM, ec-common.h:24 */
+
+void
+ec_method_config_fill(uint32_t bricks, uint32_t redundancy, ec_config_t *c)
+{
+    c->version = ECM_CONFIG_VERSION;
+    c->algorithm = ECM_CONFIG_ALGORITHM;
+    c->gf_word_size = EC_GF_BITS;
+    c->bricks = (uint8_t)bricks;
+    c->redundancy = (uint8_t)redundancy;
+    c->chunk_size = EC_METHOD_CHUNK_SIZE;
+}
+
+int32_t
+ec_method_config_pack(const ec_config_t *c, uint8_t value[8])
+{
+    uint64_t data;
+    int i;
+
+    if (!c || !value || c->version > ECM_CONFIG_VERSION)
+        return -EINVAL;
+    data = (uint64_t)c->version << 56 | (uint64_t)c->algorithm << 48 |
+           (uint64_t)c->gf_word_size << 40 | (uint64_t)c->bricks << 32 |
+           (uint64_t)c->redundancy << 24 | (uint64_t)(c->chunk_size & 0xFFFFFF);
+    for (i = 0; i < 8; i++) /* big-endian, as htobe64 */
+        value[i] = (uint8_t)(data >> (56 - 8 * i));
+    return 0;
+}
+
+int32_t
+ec_method_config_unpack(const void *value, size_t len, ec_config_t *c)
+{
+    const uint8_t *v = (const uint8_t *)value;
+    uint64_t data = 0;
+    int i;
+
+    if (!value || !c || len != 8)
+        return -EINVAL;
+    for (i = 0; i < 8; i++)
+        data = data << 8 | v[i];
+    if (data == 0)
+        return -ENODATA; /* a zero config is a missing xattr (ec-helpers.c:359) */
+    c->version = (uint32_t)(data >> 56) & 0xFF;
+    if (c->version > ECM_CONFIG_VERSION)
+        return -EINVAL;
+    c->algorithm = (uint8_t)(data >> 48);
+    c->gf_word_size = (uint8_t)(data >> 40);
+    c->bricks = (uint8_t)(data >> 32);
+    c->redundancy = (uint8_t)(data >> 24);
+    c->chunk_size = (uint32_t)(data & 0xFFFFFF);
+    return 0;
+}
+
+int32_t
+ec_method_config_check(uint32_t bricks, uint32_t redundancy, const ec_config_t *c)
+{
+    uint32_t data_bricks;
+
+    if (!c)
+        return -EINVAL;
+    if (c->version == ECM_CONFIG_VERSION && c->algorithm == ECM_CONFIG_ALGORITHM &&
+        c->gf_word_size == EC_GF_BITS && c->bricks == bricks &&
+        c->redundancy == redundancy && c->chunk_size == EC_METHOD_CHUNK_SIZE)
+        return 0;
+    /* the corruption test of ec-common.c:1162-1180 (data_bricks is computed
+     * in unsigned arithmetic there too; bricks <= redundancy is caught by
+     * the 2 * redundancy >= bricks test before it can matter) */
+    data_bricks = (uint32_t)c->bricks - c->redundancy;
+    if (c->redundancy < 1 || c->redundancy * 2 >= c->bricks || c->gf_word_size == 0 ||
+        (c->gf_word_size & (c->gf_word_size - 1)) != 0 ||
+        (uint32_t)(c->chunk_size * 8u) % (c->gf_word_size * data_bricks) != 0)
+        return -EINVAL;
+    return -ENOTSUP;
+}
+
 /* ------------------------------------------------------------ the API */
 
 int32_t

@@ -35,7 +35,8 @@ EXPORTS = (
     "ec_method_last_error", "ec_method_host_alloc", "ec_method_host_free",
     "ec_method_host_register", "ec_method_host_unregister",
     "ec_method_encode_matrix", "ec_method_inverse_matrix", "ec_method_gf_mul",
-    "ec_method_gf_div",
+    "ec_method_gf_div", "ec_method_config_fill", "ec_method_config_pack",
+    "ec_method_config_unpack", "ec_method_config_check",
 )
 
 
@@ -58,6 +59,22 @@ class MatrixList(ctypes.Structure):
 
 
 assert ctypes.sizeof(MatrixList) == 120
+
+
+class Config(ctypes.Structure):
+    """ec_config_t (ec-types.h:145-152): the trusted.ec.config fields."""
+    _fields_ = [
+        ("version", ctypes.c_uint32),
+        ("algorithm", ctypes.c_uint8),
+        ("gf_word_size", ctypes.c_uint8),
+        ("bricks", ctypes.c_uint8),
+        ("redundancy", ctypes.c_uint8),
+        ("chunk_size", ctypes.c_uint32),
+    ]
+
+    def astuple(self):
+        return (self.version, self.algorithm, self.gf_word_size, self.bricks,
+                self.redundancy, self.chunk_size)
 
 
 def _load():
@@ -104,6 +121,10 @@ def _load():
         "ec_method_inverse_matrix": (i32, [u32, vp, vp]),
         "ec_method_gf_mul": (u32, [u32, u32]),
         "ec_method_gf_div": (u32, [u32, u32]),
+        "ec_method_config_fill": (None, [u32, u32, ctypes.POINTER(Config)]),
+        "ec_method_config_pack": (i32, [ctypes.POINTER(Config), vp]),
+        "ec_method_config_unpack": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(Config)]),
+        "ec_method_config_check": (i32, [u32, u32, ctypes.POINTER(Config)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -325,3 +346,32 @@ class ECMatrixList:
 
 def sync_device(device, stream=None):
     return _check(lib.ec_method_sync_device(device, stream), "ec_method_sync_device")
+
+
+# --- on-disk format guard (trusted.ec.config) ------------------------------
+def config_fill(bricks, redundancy):
+    """The Config a write stores (ec-dir-write.c:144-151)."""
+    c = Config()
+    lib.ec_method_config_fill(bricks, redundancy, ctypes.byref(c))
+    return c
+
+
+def config_pack(config):
+    """8-byte big-endian xattr value (ec_dict_set_config)."""
+    out = (ctypes.c_uint8 * 8)()
+    _check(lib.ec_method_config_pack(ctypes.byref(config), out), "ec_method_config_pack")
+    return bytes(out)
+
+
+def config_unpack(value):
+    """Parse an xattr value (ec_dict_del_config); OSError(ENODATA) if all 0."""
+    c = Config()
+    buf = ctypes.create_string_buffer(bytes(value), len(value))
+    _check(lib.ec_method_config_unpack(buf, len(value), ctypes.byref(c)),
+           "ec_method_config_unpack")
+    return c
+
+
+def config_check(bricks, redundancy, config):
+    """ec_config_check: 0, -EINVAL (corrupted) or -ENOTSUP (other layout)."""
+    return lib.ec_method_config_check(bricks, redundancy, ctypes.byref(config))

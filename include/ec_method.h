@@ -37,6 +37,18 @@ extern "C" {
 #define EC_MI355X_MAX_NODES 31
 
 #ifndef __EC_TYPES_H__
+/* On-disk coding parameters stored in each fragment file's
+ * trusted.ec.config xattr (ec-types.h:145-152). */
+typedef struct _ec_config ec_config_t;
+struct _ec_config {
+    uint32_t version;
+    uint8_t algorithm;
+    uint8_t gf_word_size;
+    uint8_t bricks;
+    uint8_t redundancy;
+    uint32_t chunk_size;
+};
+
 /* Standalone declarations.  Inside GlusterFS, ec-types.h (included first)
  * provides the real definitions; the layout below is byte-compatible with
  * ec-types.h:549-562 (sizeof == 120 on LP64, same field offsets), which is
@@ -152,6 +164,37 @@ int32_t ec_method_heal_device(ec_matrix_list_t *list, int device, void *stream,
                               const void *const *in, uintptr_t target_mask,
                               void *const *out);
 int32_t ec_method_sync_device(int device, void *stream);
+
+/* ------------------------------------------------------------------------
+ * On-disk format guard (trusted.ec.config).
+ *
+ * The fragments this library writes are the reference's on-disk format bit
+ * for bit: config version 0 (EC_CONFIG_VERSION, ec-common.h:22), algorithm 0
+ * (the non-systematic Vandermonde code, ec-common.h:24), 8-bit GF words and
+ * 512-byte chunks.  These helpers produce and check the xattr exactly as the
+ * xlator does, so a volume coded on MI355X stays readable by CPU clients and
+ * a brick written with any other layout is refused before it is decoded.
+ * They need no GPU.
+ * --------------------------------------------------------------------- */
+
+/* The config a write stores for a volume of `bricks` = n bricks with
+ * `redundancy` = n - k (ec-dir-write.c:144-151, ec-heal.c:1268-1275). */
+void ec_method_config_fill(uint32_t bricks, uint32_t redundancy, ec_config_t *config);
+/* Serialise to the 8-byte big-endian xattr value (ec_dict_set_config,
+ * ec-helpers.c:298-330).  Returns 0, or -EINVAL for a version newer than 0. */
+int32_t ec_method_config_pack(const ec_config_t *config, uint8_t value[8]);
+/* Parse an xattr value (ec_dict_del_config, ec-helpers.c:333-380).  Returns 0,
+ * -EINVAL (length != 8 or unsupported version) or -ENODATA (all zeros: the
+ * xattr is absent, as the reference treats it). */
+int32_t ec_method_config_unpack(const void *value, size_t len, ec_config_t *config);
+/* ec_config_check (ec-common.c:1151-1195) for a volume of `bricks` bricks
+ * with `redundancy` redundancy: 0 when the fragment layout is the one this
+ * coder reads and writes, -EINVAL when the config is invalid or corrupted
+ * (redundancy < 1, 2*redundancy >= bricks, gf_word_size not a power of two,
+ * chunk bits not a multiple of word size x data bricks), -ENOTSUP when it is
+ * well formed but describes another layout or geometry. */
+int32_t ec_method_config_check(uint32_t bricks, uint32_t redundancy,
+                               const ec_config_t *config);
 
 /* ------------------------------------------------------------------------
  * Utilities.
