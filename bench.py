@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--no-extra", dest="extra", action="store_false")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--only", default=None,
-                    help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R | heal:K+R")
+                    help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R | heal:K+R | "
+                         "rmw:K+R")
     return ap.parse_args()
 
 
@@ -161,6 +162,34 @@ def run_heal(c, k, n, nbytes, steps, warmup, seed):
     return dict(kernel_s=kt, ok=ok, user=nst * CHUNK * k, alg=nst * CHUNK * (k + n - k))
 
 
+def run_writev(c, k, n, nbytes, steps, warmup, seed):
+    """Partial-stripe write: `nbytes` of user data at byte
+    1234 of a stripe, from a device buffer at an odd address, merged with the
+    old head / tail stripes and encoded by the fused kernel.  Checked against
+    the plain encoder on the materialised padded buffer."""
+    torch = c.torch
+    S = CHUNK * k
+    head = 1234 % S
+    base = rand_u8(torch, nbytes + 64, seed, c.dev)
+    user = base[13:13 + nbytes]
+    oh = rand_u8(torch, S, seed + 1, c.dev)
+    ot = rand_u8(torch, S, seed + 2, c.dev)
+    size = (head + nbytes + S - 1) // S * S
+    nst = size // S
+    outs = [torch.empty(nst * CHUNK, dtype=torch.uint8, device=c.dev) for _ in range(n)]
+    L = c.g.ECMatrixList(k, n)
+    torch.cuda.synchronize()
+    wall, kt = timed(torch, lambda: L.writev_encode_device(c.dev.index, c.sp, head, nbytes, user,
+                                                           oh, ot, outs), steps, warmup)
+    tail = size - head - nbytes
+    v = torch.cat([oh[:head], user, ot[S - tail:]])
+    ref = [torch.empty_like(o) for o in outs]
+    L.encode_device(c.dev.index, c.sp, nst, v, ref)
+    torch.cuda.synchronize()
+    ok = all(torch.equal(a, b) for a, b in zip(outs, ref))
+    return dict(kernel_s=kt, ok=ok, user=nbytes, alg=nbytes + n * nst * CHUNK)
+
+
 def run_e2e(c, k, n, nbytes, steps):
     """PCIe-inclusive: pinned host buffers in, pinned host buffers out, the
     library's pipelined H2D / kernel / D2H path (all visible GPUs)."""
@@ -251,6 +280,8 @@ def extra_configs(c, steps, warmup):
     put("selfheal_mixed16_8+4_1GiB", r, 2 * r["user"])
     r = run_heal(c, 8, 12, 1 << 30, st, warmup, 18)
     put("heal_fused_8+4_regen4_1GiB", r, r["alg"])
+    r = run_writev(c, 4, 6, (1 << 30) + 777, st, warmup, 19)
+    put("writev_rmw_4+2_1GiB_unaligned", r, r["alg"])
     torch.cuda.empty_cache()
     ex["e2e_pcie_4+2_512MiB"] = run_e2e(c, 4, 6, 512 << 20, 3)
     return ex
@@ -287,6 +318,8 @@ def only(c, spec, nbytes, steps, warmup):
         res = run_decode(c, k, n, nbytes, int(parts[2], 16), steps, warmup, 1)
     elif parts[0] == "mixed":
         res = run_mixed(c, k, n, nbytes, steps, warmup, 1)
+    elif parts[0] == "rmw":
+        res = run_writev(c, k, n, nbytes + 777, steps, warmup, 1)
     else:
         res = run_heal(c, k, n, nbytes, steps, warmup, 1)
     print(json.dumps(dict(only=spec, kernel_ms=res["kernel_s"] * 1e3, ok=res["ok"])))

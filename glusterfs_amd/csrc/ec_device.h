@@ -68,6 +68,23 @@ int ecd_sync(int device, void *stream);
 int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes,
                     const void *in, void *const *out, const uint8_t *enc_pat);
 
+/* Encode of a virtual input: the concatenation of nsegs segments
+ * (seg_ptr[i] == NULL: seg_len[i] zero bytes), nstripes*k*512 bytes in
+ * total, gathered into the pinned staging slots by the copy threads --
+ * the padded buffer of a partial-stripe write without a separate copy. */
+int ecd_encode_host_gather(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, uint32_t nsegs,
+                           const void *const *seg_ptr, const uint64_t *seg_len,
+                           void *const *out, const uint8_t *enc_pat);
+
+/* Partial-stripe write on device memory (asynchronous on `stream`): encode
+ * the padded buffer {old_head[0:head) | user[0:user_size) | old tail bytes}
+ * (NULL old stripes = zeros; one-stripe writes take both ends from old_head,
+ * or old_tail when old_head is NULL) into out[0..n), ceil((head +
+ * user_size) / (512k)) chunks each.  user may have any alignment. */
+int ecd_writev_encode_device(int device, void *stream, uint32_t k, uint32_t n, uint64_t head,
+                             uint64_t user_size, const void *user, const void *old_head,
+                             const void *old_tail, void *const *out, const uint8_t *enc_pat);
+
 /* Decode / reconstruct: frags[0..nfrags) are fragment buffers of
  * nstripes*512 bytes (NULL for fragments no pattern reads).  Output: when
  * outs is NULL, out = nstripes*rows*512 bytes, stripe-major (decoded data);

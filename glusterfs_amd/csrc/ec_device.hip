@@ -183,7 +183,10 @@ class CopyPool {
     {
         const std::vector<Piece> &p = *j.p;
         for (size_t i; (i = j.next.fetch_add(1)) < p.size();) {
-            memcpy(p[i].dst, p[i].src, p[i].n);
+            if (p[i].src)
+                memcpy(p[i].dst, p[i].src, p[i].n);
+            else
+                memset(p[i].dst, 0, p[i].n); /* gathered zero fill */
             j.done.fetch_add(1);
         }
     }
@@ -222,6 +225,27 @@ void add_copy(std::vector<CopyPool::Piece> &v, uint8_t *dst, const uint8_t *src,
     constexpr size_t kPiece = 2u << 20;
     for (size_t o = 0; o < n; o += kPiece)
         v.push_back({dst + o, src + o, std::min(kPiece, n - o)});
+}
+
+/* A virtual input made of consecutive segments (nullptr = zeros): the
+ * padded write buffer of a partial-stripe write (ec_method_writev_encode). */
+struct Seg {
+    const uint8_t *p;
+    size_t n;
+};
+
+/* Copy bytes [voff, voff + n) of the virtual input `segs` to dst. */
+void add_gather(std::vector<CopyPool::Piece> &v, uint8_t *dst, const std::vector<Seg> &segs,
+                uint64_t voff, size_t n)
+{
+    uint64_t base = 0;
+    for (const Seg &sg : segs) {
+        const uint64_t lo = std::max<uint64_t>(base, voff);
+        const uint64_t hi = std::min<uint64_t>(base + sg.n, voff + n);
+        if (lo < hi)
+            add_copy(v, dst + (lo - voff), sg.p ? sg.p + (lo - base) : nullptr, hi - lo);
+        base += sg.n;
+    }
 }
 
 /* Device-visible address of [p, p+n) when it lies in pinned, device-mapped
@@ -313,6 +337,8 @@ struct Region {
     size_t n;
     bool staged;
     size_t pin_off;
+    const std::vector<Seg> *gather = nullptr; /* input: bytes [voff, voff+n) */
+    uint64_t voff = 0;                        /* of a virtual input          */
 };
 
 struct Batch {
@@ -355,7 +381,9 @@ int run_pipeline(Stage *s, uint64_t nbatches,
             break;
         std::vector<CopyPool::Piece> pc;
         for (const Region &r : bt.in)
-            if (r.staged)
+            if (r.gather)
+                add_gather(pc, s->pin_in[slot] + r.pin_off, *r.gather, r.voff, r.n);
+            else if (r.staged)
                 add_copy(pc, s->pin_in[slot] + r.pin_off, r.host, r.n);
         g_copy_pool.run(pc);
         if ((rc = bt.launch(s->stream)) != 0 || !ok(hipEventRecord(s->done[slot], s->stream)))
@@ -382,6 +410,7 @@ inline uint8_t *kaddr(const Stage *s, int slot, const Region &r, bool out)
 struct EncodeJob {
     uint32_t k, n;
     const uint8_t *in;      /* whole user input                           */
+    const std::vector<Seg> *gather; /* or a virtual input (in == nullptr) */
     uint8_t *const *out;    /* n whole fragment buffers                   */
     const uint8_t *enc_pat; /* generic coefficients (k + n*k bytes)       */
     uint64_t s0, s1;        /* stripe range of this device                */
@@ -415,7 +444,8 @@ int run_encode_dev(int dev, const EncodeJob &j)
         return 0;
     HIPCHK(hipSetDevice(g_dev_ids[dev]));
     const uint64_t stripe_in = (uint64_t)j.k * ECD_CHUNK, cnt_all = j.s1 - j.s0;
-    const bool in_direct = mapped(j.in + j.s0 * stripe_in, cnt_all * stripe_in) != nullptr;
+    const bool in_direct =
+        !j.gather && mapped(j.in + j.s0 * stripe_in, cnt_all * stripe_in) != nullptr;
     bool out_direct[ECD_MAX_ROWS], all_direct = in_direct;
     for (uint32_t i = 0; i < j.n; ++i) {
         out_direct[i] = mapped(j.out[i] + j.s0 * ECD_CHUNK, cnt_all * ECD_CHUNK) != nullptr;
@@ -434,8 +464,11 @@ int run_encode_dev(int dev, const EncodeJob &j)
     if (rc == 0)
         rc = run_pipeline(s, nb, [&](uint64_t b, int slot, Batch &bt) {
             const uint64_t a = j.s0 + b * B, cnt = std::min(B, j.s1 - a);
-            bt.in.push_back({const_cast<uint8_t *>(j.in) + a * stripe_in, cnt * stripe_in,
-                             !in_direct, 0});
+            if (j.gather)
+                bt.in.push_back({nullptr, cnt * stripe_in, true, 0, j.gather, a * stripe_in});
+            else
+                bt.in.push_back({const_cast<uint8_t *>(j.in) + a * stripe_in, cnt * stripe_in,
+                                 !in_direct, 0});
             for (uint32_t i = 0; i < j.n; ++i)
                 bt.out.push_back({j.out[i] + a * ECD_CHUNK, cnt * ECD_CHUNK, !out_direct[i],
                                   (size_t)i * B * ECD_CHUNK});
@@ -678,8 +711,8 @@ int ecd_sync(int device, void *stream)
     return 0;
 }
 
-int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const void *in,
-                    void *const *out, const uint8_t *enc_pat)
+static int encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const void *in,
+                       const std::vector<Seg> *gather, void *const *out, const uint8_t *enc_pat)
 {
     if (ecd_device_count() == 0)
         return -ENODEV;
@@ -687,6 +720,7 @@ int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const v
     base.k = k;
     base.n = n;
     base.in = static_cast<const uint8_t *>(in);
+    base.gather = gather;
     base.out = reinterpret_cast<uint8_t *const *>(out);
     base.enc_pat = enc_pat;
     return partition(ndev, nstripes, 1, nstripes * ECD_CHUNK * (k + n),
@@ -696,6 +730,79 @@ int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const v
         j.s1 = s1;
         return run_encode_dev(d, j);
     });
+}
+
+int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const void *in,
+                    void *const *out, const uint8_t *enc_pat)
+{
+    return encode_host(ndev, k, n, nstripes, in, nullptr, out, enc_pat);
+}
+
+int ecd_encode_host_gather(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, uint32_t nsegs,
+                           const void *const *seg_ptr, const uint64_t *seg_len,
+                           void *const *out, const uint8_t *enc_pat)
+{
+    std::vector<Seg> segs;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < nsegs; ++i) {
+        segs.push_back({static_cast<const uint8_t *>(seg_ptr[i]), seg_len[i]});
+        total += seg_len[i];
+    }
+    if (total != nstripes * k * ECD_CHUNK)
+        return -EINVAL;
+    return encode_host(ndev, k, n, nstripes, nullptr, &segs, out, enc_pat);
+}
+
+int ecd_writev_encode_device(int device, void *stream, uint32_t k, uint32_t n, uint64_t head,
+                             uint64_t user_size, const void *user, const void *old_head,
+                             const void *old_tail, void *const *out, const uint8_t *enc_pat)
+{
+    if (ecd_device_count() <= device || device < 0)
+        return -ENODEV;
+    const uint64_t S = (uint64_t)k * ECD_CHUNK;
+    if (head >= S || user_size == 0 || !user)
+        return -EINVAL;
+    const uint64_t b1 = head, b2 = head + user_size, nst = (b2 + S - 1) / S;
+    const uint8_t *u = static_cast<const uint8_t *>(user);
+    const uint8_t *hs = static_cast<const uint8_t *>(old_head);
+    const uint8_t *ts = static_cast<const uint8_t *>(old_tail);
+    /* one stripe: its old content (either pointer) fills both ends, as
+     * ec_merge_stripe_head_locked does (ec-inode-write.c:1886-1895) */
+    if (nst == 1) {
+        hs = hs ? hs : ts;
+        ts = hs ? hs + b2 : nullptr;
+    } else if (ts) {
+        ts += b2 - (nst - 1) * S; /* ec_merge_stripe_tail_locked, :1898-1908 */
+    }
+    HIPCHK(hipSetDevice(g_dev_ids[device]));
+    hipStream_t st = pick_stream(stream);
+    const bool fused = ecdk_has_vander(k, n);
+    const uint64_t scratch = fused ? (nst == 1 ? 1 : 2) * S : nst * S;
+    uint8_t *buf = nullptr;
+    HIPCHK(hipMallocAsync(reinterpret_cast<void **>(&buf), scratch, st));
+    int rc;
+    if (fused) {
+        rc = ecdk_rmw_gather(st, hs, u, ts, b1, b2, 0, S, buf);
+        if (rc == 0 && nst > 1)
+            rc = ecdk_rmw_gather(st, hs, u, ts, b1, b2, (nst - 1) * S, S, buf + S);
+        if (rc == 0)
+            rc = ecdk_encode_vander_rmw(st, k, n, nst, buf, u - head, out);
+    } else {
+        rc = ecdk_rmw_gather(st, hs, u, ts, b1, b2, 0, nst * S, buf);
+        if (rc == 0) {
+            EncodeJob j{};
+            j.k = k;
+            j.n = n;
+            j.enc_pat = enc_pat;
+            rc = launch_encode(st, j, buf, reinterpret_cast<uint8_t *const *>(out), nst);
+        }
+    }
+    const hipError_t fe = hipFreeAsync(buf, st);
+    if (rc == 0 && fe != hipSuccess) {
+        set_err("hipFreeAsync", fe);
+        rc = -EIO;
+    }
+    return rc;
 }
 
 int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, uint32_t nfrags,

@@ -88,6 +88,52 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
     return -ENOTSUP;
 }
 
+int ecdk_rmw_gather(hipStream_t s, const uint8_t *head, const uint8_t *user, const uint8_t *tail,
+                    uint64_t b1, uint64_t b2, uint64_t o0, uint64_t n, uint8_t *dst)
+{
+    if (n % 16 || ((uintptr_t)dst & 15))
+        return -EINVAL;
+    const uint64_t g = (n / 16 + kBlock - 1) / kBlock;
+    if (g == 0)
+        return 0;
+    if (g > 0x7fffffffull)
+        return -EINVAL;
+    RmwSrc v{head, user, tail, b1, b2};
+    hipLaunchKernelGGL(ec_rmw_gather, dim3((u32)g), dim3(kBlock), 0, s, v, o0, n, dst);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+template <int K, int N, int W>
+int launch_vander_rmw(hipStream_t s, uint64_t nstripes, const uint8_t *edge,
+                      const uint8_t *user_shift, void *const *out)
+{
+    FragPtrs f;
+    for (int i = 0; i < N; ++i)
+        f.p[i] = static_cast<uint8_t *>(out[i]);
+    const uint64_t g = vander_grid<W>(nstripes);
+    if (g == 0)
+        return 0;
+    if (g > 0x7fffffffull)
+        return -EINVAL;
+    hipLaunchKernelGGL((ec_encode_vander_rmw<K, N, W>), dim3((u32)g), dim3(kBlock), 0, s, edge,
+                       user_shift, f, nstripes);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ecdk_encode_vander_rmw(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
+                           const uint8_t *edge, const uint8_t *user_shift, void *const *out)
+{
+    if (k == 2 && n == 3)
+        return launch_vander_rmw<2, 3, 4>(s, nstripes, edge, user_shift, out);
+    if (k == 4 && n == 6)
+        return launch_vander_rmw<4, 6, 2>(s, nstripes, edge, user_shift, out);
+    if (k == 8 && n == 12)
+        return launch_vander_rmw<8, 12, 1>(s, nstripes, edge, user_shift, out);
+    if (k == 16 && n == 20)
+        return launch_vander_rmw<16, 20, 1>(s, nstripes, edge, user_shift, out);
+    return -ENOTSUP;
+}
+
 /* Re-lay the packed byte patterns {src[k], coef[rows][k]} out in words. */
 int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
 {

@@ -435,6 +435,118 @@ inline size_t combine_lds(u32 k)
     return (size_t)k * 8 * TS * ECD_CHUNK;
 }
 
+/* ------------------------------------------- partial-stripe writes (RMW) */
+
+/* The padded write buffer of ec_writev_prepare_buffers (ec-inode-write.c:
+ * 1825-1848) merged with the old head / tail stripe (ec_merge_stripe_head /
+ * _tail_locked, :1883-1908), described instead of materialised: byte v of
+ * the virtual input is seg[0] for v < b1 (old head bytes, nullptr = zeros),
+ * user[v - b1] for b1 <= v < b2, and seg[2][v - b2] after (old tail bytes or
+ * zeros).  `user` has arbitrary byte alignment. */
+struct RmwSrc {
+    const uint8_t *head, *user, *tail;
+    uint64_t b1, b2;
+};
+
+__device__ __forceinline__ uint8_t rmw_byte(const RmwSrc &v, uint64_t o)
+{
+    if (o < v.b1)
+        return v.head ? v.head[o] : 0;
+    if (o < v.b2)
+        return v.user[o - v.b1];
+    return v.tail ? v.tail[o - v.b2] : 0;
+}
+
+/* W dwords of `p`, which may have any byte alignment: the aligned dwords
+ * that cover [p, p + 4W) are loaded and funnel-shifted with v_alignbyte_b32.
+ * Every loaded dword holds at least one byte of the range, so no load can
+ * cross into a page the range does not touch. */
+template <int W>
+__device__ __forceinline__ void load_plane_unaligned(const uint8_t *p, u32 (&d)[W])
+{
+    const u32 mis = (u32)((uintptr_t)p & 3u);
+    const u32 *a = reinterpret_cast<const u32 *>((uintptr_t)p & ~(uintptr_t)3);
+    if (mis == 0) {
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            d[w] = a[w];
+        return;
+    }
+    u32 t[W + 1];
+#pragma unroll
+    for (int w = 0; w <= W; ++w)
+        t[w] = a[w];
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+        d[w] = __builtin_amdgcn_alignbyte(t[w + 1], t[w], mis);
+}
+
+/* Materialise bytes [o0, o0 + n) of the virtual input into dst (16 bytes
+ * per thread; n a multiple of 16).  Interior pieces take the realigned
+ * dword path, the <= 2 pieces that straddle a segment boundary go byte by
+ * byte. */
+__global__ __launch_bounds__(kBlock) void ec_rmw_gather(const RmwSrc v, uint64_t o0, uint64_t n,
+                                                        uint8_t *__restrict__ dst)
+{
+    const uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 16;
+    if (i >= n)
+        return;
+    const uint64_t o = o0 + i;
+    u32 d[4];
+    if (o >= v.b1 && o + 16 <= v.b2) {
+        load_plane_unaligned<4>(v.user + (o - v.b1), d);
+    } else {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            u32 x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                x |= (u32)rmw_byte(v, o + 4 * w + b) << (8 * b);
+            d[w] = x;
+        }
+    }
+    *reinterpret_cast<uint4 *>(dst + i) = make_uint4(d[0], d[1], d[2], d[3]);
+}
+
+/* Fused partial-stripe encode for the compile-time Vandermonde geometries:
+ * stripe 0 and stripe nst-1 (the merged boundary stripes, gathered into
+ * `edge` by ec_rmw_gather: edge + 0 and edge + (nedge-1)*stripe) are read
+ * aligned; every interior stripe t is read straight from the caller's
+ * buffer at user + t*stripe - head with realigned loads, so the interior is
+ * never copied (the reference memcpy's the whole write first,
+ * ec-inode-write.c:1844). */
+template <int K, int N, int W>
+__global__ __launch_bounds__(kBlock) void ec_encode_vander_rmw(const uint8_t *__restrict__ edge,
+                                                               const uint8_t *user_shift,
+                                                               const FragPtrs out,
+                                                               uint64_t nstripes)
+{
+    constexpr int L = 16 / W;
+    constexpr uint64_t S = (uint64_t)K * ECD_CHUNK;
+    const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t stripe = gtid / L;
+    if (stripe >= nstripes)
+        return;
+    const u32 colb = (u32)(gtid % L) * (4 * W);
+    u32 x[K][8][W];
+    if (stripe == 0 || stripe == nstripes - 1) {
+        const uint8_t *s = edge + (stripe == 0 ? 0 : (nstripes > 1 ? S : 0)) + colb;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            load_chunk<W>(s + j * ECD_CHUNK, x[j]);
+    } else {
+        /* user_shift = user - head: the virtual offset of user byte 0 is head */
+        const uint8_t *s = user_shift + stripe * S + colb;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane_unaligned<W>(s + j * ECD_CHUNK + b * 64, x[j][b]);
+    }
+    encode_rows<K, W, false>(std::make_integer_sequence<int, N>{}, x, out,
+                             stripe * (uint64_t)ECD_CHUNK + colb);
+}
+
 } // namespace ecdev
 
 #endif

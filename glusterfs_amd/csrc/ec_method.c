@@ -839,6 +839,75 @@ ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
                            pat, NULL, 0);
 }
 
+/* ------------------------------------------------- partial-stripe writes */
+
+int32_t
+ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iovec *iov,
+                        int count, const void *old_head, const void *old_tail,
+                        void *const *out)
+{
+    ecm_ctx_t *ctx;
+    const void *segp[3 + 64];
+    uint64_t segl[3 + 64], user = 0, S, b2, nst;
+    const uint8_t *hs = (const uint8_t *)old_head, *ts = (const uint8_t *)old_tail;
+    uint32_t ns = 0, i;
+    int c, dev;
+
+    if (!list || !(ctx = CTX(list)) || !out || count < 0 || count > 64 || (count && !iov))
+        return -EINVAL;
+    S = list->stripe;
+    if (head >= S)
+        return -EINVAL;
+    for (c = 0; c < count; c++)
+        user += iov[c].iov_len;
+    if (user == 0)
+        return 0;
+    b2 = head + user;
+    nst = (b2 + S - 1) / S;
+    /* device buffers: the fused kernel (one contiguous user buffer) */
+    dev = ecd_ptr_device(iov[0].iov_base);
+    if (dev >= 0) {
+        if (count != 1)
+            return -EINVAL;
+        c = ec_method_writev_encode_device(list, dev, NULL, head, user, iov[0].iov_base,
+                                           old_head, old_tail, out);
+        return c ? c : ecd_sync(dev, NULL);
+    }
+    for (i = 0; i < ctx->n; i++)
+        if (ecd_ptr_device(out[i]) >= 0)
+            return -EINVAL;
+    if (nst == 1) { /* one stripe: its old content fills both ends */
+        hs = hs ? hs : ts;
+        ts = hs ? hs + b2 : NULL;
+    } else if (ts) {
+        ts += b2 - (nst - 1) * S;
+    }
+    segp[ns] = hs;
+    segl[ns++] = head;
+    for (c = 0; c < count; c++) {
+        segp[ns] = iov[c].iov_base;
+        segl[ns++] = iov[c].iov_len;
+    }
+    segp[ns] = ts;
+    segl[ns++] = nst * S - b2;
+    return ecd_encode_host_gather(0, ctx->k, ctx->n, nst, ns, segp, segl, out, ctx->enc_pat);
+}
+
+int32_t
+ec_method_writev_encode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t head,
+                               uint64_t size, const void *user, const void *old_head,
+                               const void *old_tail, void *const *out)
+{
+    ecm_ctx_t *ctx;
+
+    if (!list || !(ctx = CTX(list)) || !out)
+        return -EINVAL;
+    if (size == 0)
+        return 0;
+    return ecd_writev_encode_device(device, stream, ctx->k, ctx->n, head, size, user, old_head,
+                                    old_tail, out, ctx->enc_pat);
+}
+
 /* ---------------------------------------------------- device-resident */
 
 static void

@@ -36,7 +36,8 @@ EXPORTS = (
     "ec_method_host_register", "ec_method_host_unregister",
     "ec_method_encode_matrix", "ec_method_inverse_matrix", "ec_method_gf_mul",
     "ec_method_gf_div", "ec_method_config_fill", "ec_method_config_pack",
-    "ec_method_config_unpack", "ec_method_config_check",
+    "ec_method_config_unpack", "ec_method_config_check", "ec_method_writev_encode",
+    "ec_method_writev_encode_device",
 )
 
 
@@ -59,6 +60,19 @@ class MatrixList(ctypes.Structure):
 
 
 assert ctypes.sizeof(MatrixList) == 120
+
+
+class _IOVec(ctypes.Structure):
+    _fields_ = [("iov_base", ctypes.c_void_p), ("iov_len", ctypes.c_size_t)]
+
+
+def _nbytes(buf):
+    """Byte length of a numpy array / torch tensor / bytes-like buffer."""
+    if hasattr(buf, "nbytes"):
+        return int(buf.nbytes)
+    if hasattr(buf, "numel"):
+        return int(buf.numel() * buf.element_size())
+    return len(buf)
 
 
 class Config(ctypes.Structure):
@@ -121,6 +135,9 @@ def _load():
         "ec_method_inverse_matrix": (i32, [u32, vp, vp]),
         "ec_method_gf_mul": (u32, [u32, u32]),
         "ec_method_gf_div": (u32, [u32, u32]),
+        "ec_method_writev_encode": (i32, [P, u64, vp, ctypes.c_int, vp, vp, vp]),
+        "ec_method_writev_encode_device": (i32, [P, ctypes.c_int, vp, u64, u64, vp, vp, vp,
+                                                 vp]),
         "ec_method_config_fill": (None, [u32, u32, ctypes.POINTER(Config)]),
         "ec_method_config_pack": (i32, [ctypes.POINTER(Config), vp]),
         "ec_method_config_unpack": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(Config)]),
@@ -313,6 +330,20 @@ class ECMatrixList:
         return _check(lib.ec_method_decode_mixed(ctypes.byref(self._list), nstripes,
                                                  group_stripes, gm, _ptr_array(frags),
                                                  addr(out)), "ec_method_decode_mixed")
+
+    def writev_encode(self, head, user, old_head, old_tail, out):
+        """ec_method_writev_encode: `user` is one buffer or a list of buffers
+        (the writev iovec list); old_head / old_tail may be None."""
+        bufs = user if isinstance(user, (list, tuple)) else [user]
+        iov = (_IOVec * len(bufs))(*[_IOVec(addr(b), _nbytes(b)) for b in bufs])
+        return _check(lib.ec_method_writev_encode(ctypes.byref(self._list), head, iov,
+                                                  len(bufs), addr(old_head), addr(old_tail),
+                                                  _ptr_array(out)), "ec_method_writev_encode")
+
+    def writev_encode_device(self, device, stream, head, size, user, old_head, old_tail, out):
+        return _check(lib.ec_method_writev_encode_device(
+            ctypes.byref(self._list), device, stream, head, size, addr(user), addr(old_head),
+            addr(old_tail), _ptr_array(out)), "ec_method_writev_encode_device")
 
     def heal(self, nstripes, mask, inp, target_mask, out):
         return _check(lib.ec_method_heal(ctypes.byref(self._list), nstripes, mask,

@@ -19,6 +19,7 @@
 #include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <sys/uio.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -140,6 +141,28 @@ int32_t ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask
                        const void *const *in, uintptr_t target_mask,
                        void *const *out);
 
+/* Partial-stripe write: the read-modify-write of
+ * ec_writev_start (ec-inode-write.c:1987-2085) fused with ec_writev_encode.
+ * The write's user data is the iovec list iov[0..count) (as the writev fop
+ * carries it) and starts `head` bytes into its first stripe (fop->head =
+ * offset % stripe, ec-inode-write.c:1833).  The encoded range is the
+ * padded buffer of ec_writev_prepare_buffers (:1825-1848):
+ *   bytes [0, head)                 old_head[0, head)      (head merge, :1883)
+ *   bytes [head, head + user bytes) the user data
+ *   the rest of the last stripe     the same bytes of old_tail (tail merge,
+ *                                   :1898-1908)
+ * old_head / old_tail are the current (decoded) contents of the first / last
+ * stripe -- from the stripe cache or a read -- or NULL beyond end of file
+ * (zeros, :2007-2008).  When the write lies in one stripe its old content
+ * fills both ends (old_head, or old_tail when old_head is NULL).  out[i]
+ * receives ceil((head + user bytes) / (512k)) chunks of fragment i.  The
+ * merge happens in the staging copy for host buffers and inside the
+ * kernel for device buffers (count must be 1 there); the interior of the
+ * write is never copied separately.  Returns 0 or -errno. */
+int32_t ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iovec *iov,
+                                int count, const void *old_head, const void *old_tail,
+                                void *const *out);
+
 /* Device-resident, asynchronous variants for callers that keep stripes in
  * MI355X memory: all buffers are device pointers on `device` (index among
  * the visible gfx950 devices), work is queued on `stream` (a hipStream_t;
@@ -163,6 +186,10 @@ int32_t ec_method_heal_device(ec_matrix_list_t *list, int device, void *stream,
                               uint64_t nstripes, uintptr_t mask,
                               const void *const *in, uintptr_t target_mask,
                               void *const *out);
+int32_t ec_method_writev_encode_device(ec_matrix_list_t *list, int device, void *stream,
+                                       uint64_t head, uint64_t size, const void *user,
+                                       const void *old_head, const void *old_tail,
+                                       void *const *out);
 int32_t ec_method_sync_device(int device, void *stream);
 
 /* ------------------------------------------------------------------------

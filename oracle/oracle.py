@@ -144,3 +144,34 @@ def decode(k, rows, frags, nthreads=1):
 def mask_rows(mask):
     """Brick mask -> ascending rows (brick_idx + 1), like ec-inode-read.c:1174."""
     return [i + 1 for i in range(64) if (mask >> i) & 1]
+
+
+def writev_merge(k, head, user, old_head=None, old_tail=None):
+    """The padded buffer a partial-stripe write encodes (test infrastructure).
+
+    Restates ec_writev_prepare_buffers (ec-inode-write.c:1825-1848: a buffer
+    of roundup(head + user, stripe) bytes with the user data at `head`),
+    the zero fill beyond end of file (ec_writev_start, :2007-2008, :2031)
+    and the old-stripe merges ec_merge_stripe_head_locked (:1883-1895: the
+    head bytes and, for a one-stripe write, the bytes after the user data)
+    and ec_merge_stripe_tail_locked (:1898-1908: the last `tail` bytes of the
+    last stripe).  old_head / old_tail are stripe-sized arrays or None.
+    """
+    S = CHUNK * k
+    user = np.asarray(user, dtype=np.uint8)
+    us = user.size
+    size = (head + us + S - 1) // S * S
+    v = np.zeros(size, np.uint8)
+    v[head:head + us] = user
+    if size == S:
+        old = old_head if old_head is not None else old_tail
+        if old is not None:
+            v[:head] = old[:head]
+            v[head + us:] = old[head + us:S]
+    else:
+        if old_head is not None:
+            v[:head] = old_head[:head]
+        if old_tail is not None:
+            tail = size - (head + us)
+            v[head + us:] = old_tail[S - tail:S]
+    return v

@@ -181,3 +181,26 @@ def test_xorshift_known_start(oracle):
         x ^= (x << 17) & 0xFFFFFFFFFFFFFFFF
         want.append(x)
     assert buf.tolist() == want
+
+
+def test_writev_merge_pinned_by_hand(oracle):
+    """oracle.writev_merge against byte positions worked out by hand from
+    ec_writev_prepare_buffers / ec_merge_stripe_{head,tail}_locked
+    (ec-inode-write.c:1825-1908) for a 2+1 volume (stripe 1024)."""
+    import numpy as np
+    S = 1024
+    oh = np.arange(S, dtype=np.uint32).astype(np.uint8)
+    ot = (255 - np.arange(S, dtype=np.uint32)).astype(np.uint8)
+    user = np.full(50, 7, np.uint8)
+    v = oracle.writev_merge(2, 1000, user, oh, ot)       # spans two stripes
+    assert v.size == 2048
+    assert np.array_equal(v[:1000], oh[:1000])
+    assert np.array_equal(v[1000:1050], user)
+    assert np.array_equal(v[1050:], ot[26:])               # tail = 998 bytes
+    v = oracle.writev_merge(2, 10, user, oh, ot)          # one stripe: both ends old_head
+    assert v.size == S and np.array_equal(v[:10], oh[:10])
+    assert np.array_equal(v[60:], oh[60:])
+    v = oracle.writev_merge(2, 0, user, None, ot)         # head 0: tail from old_tail
+    assert np.array_equal(v[50:], ot[50:])
+    v = oracle.writev_merge(2, 10, user, None, None)      # beyond EOF: zeros
+    assert v[:10].sum() == 0 and v[60:].sum() == 0
