@@ -276,6 +276,8 @@ def extra_configs(c, steps, warmup):
     put("dec_8+4_0xFF0_1GiB", r, 2 * r["user"])
     r = run_encode(c, 16, 20, 2 << 30, st, warmup, 15)
     put("enc_16+4_2GiB", r, 2.25 * r["user"])
+    r = run_decode(c, 16, 20, 1 << 30, 0xFFFF0, st, warmup, 20)
+    put("dec_16+4_0xFFFF0_1GiB", r, 2 * r["user"])
     r = run_mixed(c, 8, 12, 1 << 30, st, warmup, 17)
     put("selfheal_mixed16_8+4_1GiB", r, 2 * r["user"])
     r = run_heal(c, 8, 12, 1 << 30, st, warmup, 18)
@@ -284,6 +286,7 @@ def extra_configs(c, steps, warmup):
     put("writev_rmw_4+2_1GiB_unaligned", r, r["alg"])
     torch.cuda.empty_cache()
     ex["e2e_pcie_4+2_512MiB"] = run_e2e(c, 4, 6, 512 << 20, 3)
+    ex["e2e_pcie_16+4_512MiB"] = run_e2e(c, 16, 20, 512 << 20, 3)
     return ex
 
 

@@ -4,9 +4,13 @@
  *
  * Shipped configuration (tools/kbench A/B runs, profiles/kbench_r01.log):
  *   encode   compile-time Vandermonde rows for 2+1, 4+2, 8+4, 16+4;
- *            W = 4 / 2 / 1 / 1 dwords per plane per lane (VGPR budget);
- *            non-temporal stores for 16+4 only (+2.5 %; neutral or worse
- *            elsewhere)
+ *            W = 4 / 2 / 1 / 1 dwords per plane per lane (VGPR budget)
+ *   stores   non-temporal for k > 4 (encode and combine), default for
+ *            k <= 4 (profiles/kbench_r01_nts.log).  Without them the
+ *            output lines sit dirty in the per-XCD L2 and are written back
+ *            at the kernel boundary: 8+4 decode of a 64K-stripe batch
+ *            (BASELINE configs[2]) 0.58 -> 0.70 of 8 TB/s, 8+4 encode
+ *            0.655 -> 0.670; at k = 4 they cost 3-8 %
  *   combine  one tile per block, staged by LDS-DMA (global_load_lds_dwordx4):
  *            k <= 4: 16-stripe tiles, 4 waves; k > 4: 8-stripe tiles (LDS per
  *            block caps occupancy), 8 waves -- measured (profiles/kbench_r01_*)
@@ -57,11 +61,12 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
     if (g > 0x7fffffffull)
         return -EINVAL;
     const size_t lds = combine_lds<TS>(a.k);
+    constexpr bool NTS = K > 4;
     if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, true, false, true>), dim3((u32)g),
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, true, NTS, true>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
     else
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, false, true>), dim3((u32)g),
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS, true>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
@@ -82,7 +87,7 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
     if (k == 4 && n == 6)
         return launch_vander<4, 6, 2>(s, nstripes, in, out, zc);
     if (k == 8 && n == 12)
-        return launch_vander<8, 12, 1>(s, nstripes, in, out, zc);
+        return launch_vander<8, 12, 1, true>(s, nstripes, in, out, zc);
     if (k == 16 && n == 20)
         return launch_vander<16, 20, 1, true>(s, nstripes, in, out, zc);
     return -ENOTSUP;

@@ -299,7 +299,8 @@ __device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
  * GLDS: stage the tile with LDS-DMA (global_load_lds_dwordx4, no VGPRs)
  * instead of global_load + ds_write; PF: issue the next input's LDS reads
  * before each multiply. */
-template <int K, int TS, int NW, bool MIXED, bool NTS, bool GLDS = false, bool PF = false>
+template <int K, int TS, int NW, bool MIXED, bool NTS, bool GLDS = false, bool PF = false,
+          bool PP = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -395,31 +396,150 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                 d[b][1] = t.y;
             }
         };
-        if constexpr (PF)
-            read_input(0, y);
-        for (u32 p = 0; p < k; ++p) {
+        auto coef = [&](u32 p) {
             const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
-            const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
-            if constexpr (PF) {
-                /* issue the next input's LDS reads before this multiply */
-                u32 yn[8][CW];
-                read_input(p + 1 < k ? p + 1 : p, yn);
-                ecgf::mul_xor_rt<CW>(c, acc, y);
+            return __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
+        };
+        if constexpr (PP) {
+            /* ping-pong accumulators (ecgf::mul_xor_rt_pp): acc -> y2 -> acc */
+            u32 acc2[8][CW];
+            for (u32 p = 0; p < k; p += 2) {
+                const u32 c0 = coef(p);
+                if (c0)
+                    read_input(p, y);
+                ecgf::mul_xor_rt_pp<CW>(c0, acc, acc2, y);
+                const u32 c1 = p + 1 < k ? coef(p + 1) : 0u;
+                if (c1)
+                    read_input(p + 1, y);
+                ecgf::mul_xor_rt_pp<CW>(c1, acc2, acc, y);
+            }
+        } else {
+            if constexpr (PF)
+                read_input(0, y);
+            for (u32 p = 0; p < k; ++p) {
+                const u32 c = coef(p);
+                if constexpr (PF) {
+                    /* issue the next input's LDS reads before this multiply */
+                    u32 yn[8][CW];
+                    read_input(p + 1 < k ? p + 1 : p, yn);
+                    ecgf::mul_xor_rt<CW>(c, acc, y);
 #pragma unroll
-                for (int b = 0; b < 8; ++b)
+                    for (int b = 0; b < 8; ++b)
 #pragma unroll
-                    for (int w = 0; w < CW; ++w)
-                        y[b][w] = yn[b][w];
-            } else {
-                if (c == 0)
-                    continue;
-                read_input(p, y);
-                ecgf::mul_xor_rt<CW>(c, acc, y);
+                        for (int w = 0; w < CW; ++w)
+                            y[b][w] = yn[b][w];
+                } else {
+                    if (c == 0)
+                        continue;
+                    read_input(p, y);
+                    ecgf::mul_xor_rt<CW>(c, acc, y);
+                }
             }
         }
         const uint64_t ost = t0 + s;
         if (ost < a.nstripes)
             store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+    }
+}
+
+/* ec_combine for wide codes (k > G): the tile's inputs are staged and
+ * consumed in groups of G fragments through one G-input LDS buffer, the
+ * output rows accumulating in VGPRs across groups (wave w owns items w,
+ * w + NW, ...; at most IPW each).  LDS per block drops from k to G inputs,
+ * so more blocks share a CU and one block's XOR-heavy compute phase overlaps
+ * other blocks' loads and stores -- at k = 16 the single-phase kernel holds
+ * 2 blocks per CU and runs its memory and VALU phases nearly back to back. */
+template <int K, int G, int NW, int IPW, bool MIXED, bool NTS>
+__global__ __launch_bounds__(NW * 64) void ec_combine_grouped(const CombineArgs a)
+{
+    constexpr u32 T = 8;                 /* stripes per tile                   */
+    constexpr int CW = 2;
+    constexpr u32 NI = G * T * 32 / 64;  /* LDS-DMA wave instructions / group */
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const u32 cs = lane >> 3, cc = lane & 7u;
+    const u32 rot = (cs & 3u) << 6;
+    const uint8_t *col = lds + cs * ECD_CHUNK + cc * 8u;
+
+    u32 pb = 0;
+    if constexpr (MIXED)
+        pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
+
+    u32 acc[IPW][8][CW];
+#pragma unroll
+    for (int j = 0; j < IPW; ++j)
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int w = 0; w < CW; ++w)
+                acc[j][b][w] = 0;
+
+    for (u32 g0 = 0; g0 < k; g0 += G) {
+        if (g0)
+            __syncthreads();             /* everyone is done with the buffer */
+#pragma unroll
+        for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
+            const u32 ins = j * NW + wave;
+            if (ins >= NI)
+                break;
+            const u32 p = g0 + ins / (T / 2);
+            if (p >= k)
+                break;
+            const u32 e = ins * 64 + lane;
+            const u32 s = (e / 32) % T, slot = e & 31u;
+            const uint64_t st = t0 + s;
+            if (st < a.nstripes) {
+                const u32 src = pat_byte(a, pb, p);
+                const uint8_t *gp = a.in_base[src] + st * a.in_stride +
+                                    ((((slot >> 2) ^ (s & 3u)) << 6) | ((slot & 3u) << 4));
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)gp,
+                    (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+            }
+        }
+        __syncthreads();
+        const u32 ng = k - g0 < (u32)G ? k - g0 : (u32)G;
+        /* the items' coefficient words for this group (<= 2 words each) */
+        u32 cw[IPW][2];
+        static_for<0, IPW>([&](auto jj) {
+            constexpr int j = decltype(jj)::value;
+            const u32 r = wave + (u32)j * NW;
+            const u32 rw = pb + a.kw * (1 + (r < a.rows ? r : 0)) + (g0 >> 2);
+            cw[j][0] = a.pat[rw];
+            cw[j][1] = G > 4 ? a.pat[rw + 1] : 0u;
+        });
+        for (u32 q = 0; q < ng; ++q) {
+            /* one LDS read of input q serves all of this wave's rows */
+            u32 y[8][CW];
+            const uint8_t *src = col + q * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint2 t = *reinterpret_cast<const uint2 *>(src + (((u32)b << 6) ^ rot));
+                y[b][0] = t.x;
+                y[b][1] = t.y;
+            }
+            static_for<0, IPW>([&](auto jj) {
+                constexpr int j = decltype(jj)::value;
+                const u32 wsel = q < 4 ? cw[j][0] : cw[j][1];
+                u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((q & 3u) * 8u)) & 0xFFu);
+                if (wave + (u32)j * NW >= a.rows)
+                    c = 0;
+                ecgf::mul_xor_rt<CW>(c, acc[j], y);
+            });
+        }
+    }
+    const uint64_t ost = t0 + cs;
+    if (ost < a.nstripes) {
+        static_for<0, IPW>([&](auto jj) {
+            constexpr int j = decltype(jj)::value;
+            const u32 r = wave + (u32)j * NW;
+            if (r < a.rows)
+                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc[j]);
+        });
     }
 }
 
