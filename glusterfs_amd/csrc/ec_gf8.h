@@ -131,47 +131,6 @@ __device__ __forceinline__ void mul_xor_rt(u32 c, u32 (&acc)[8][W], const u32 (&
     }
 }
 
-/* out = in ^ c*x for a wave-uniform run-time c; c == 0 copies.  Used in
- * ping-pong pairs (A -> B, then B -> A): when one accumulator is updated in
- * place inside a loop, the register allocator gives the 255 cases' results
- * fresh VGPRs and copies them back at the join (16 v_mov per multiply at
- * W = 2, a third of the VALU work); with distinct in/out values every case
- * writes the same out registers and the join needs no copies. */
-template <int W>
-__device__ __forceinline__ void mul_xor_rt_pp(u32 c, const u32 (&in)[8][W], u32 (&out)[8][W],
-                                              const u32 (&x)[8][W])
-{
-    switch (c) {
-#define ECGF_CASE(n)                                                           \
-    case n:                                                                    \
-        mul_xor<n, W>(out, in, x);                                             \
-        break;
-#define ECGF_CASE16(h)                                                         \
-    ECGF_CASE(h * 16 + 0) ECGF_CASE(h * 16 + 1) ECGF_CASE(h * 16 + 2)          \
-    ECGF_CASE(h * 16 + 3) ECGF_CASE(h * 16 + 4) ECGF_CASE(h * 16 + 5)          \
-    ECGF_CASE(h * 16 + 6) ECGF_CASE(h * 16 + 7) ECGF_CASE(h * 16 + 8)          \
-    ECGF_CASE(h * 16 + 9) ECGF_CASE(h * 16 + 10) ECGF_CASE(h * 16 + 11)        \
-    ECGF_CASE(h * 16 + 12) ECGF_CASE(h * 16 + 13) ECGF_CASE(h * 16 + 14)       \
-    ECGF_CASE(h * 16 + 15)
-        ECGF_CASE(1) ECGF_CASE(2) ECGF_CASE(3) ECGF_CASE(4) ECGF_CASE(5)
-        ECGF_CASE(6) ECGF_CASE(7) ECGF_CASE(8) ECGF_CASE(9) ECGF_CASE(10)
-        ECGF_CASE(11) ECGF_CASE(12) ECGF_CASE(13) ECGF_CASE(14) ECGF_CASE(15)
-        ECGF_CASE16(1) ECGF_CASE16(2) ECGF_CASE16(3) ECGF_CASE16(4)
-        ECGF_CASE16(5) ECGF_CASE16(6) ECGF_CASE16(7) ECGF_CASE16(8)
-        ECGF_CASE16(9) ECGF_CASE16(10) ECGF_CASE16(11) ECGF_CASE16(12)
-        ECGF_CASE16(13) ECGF_CASE16(14) ECGF_CASE16(15)
-#undef ECGF_CASE16
-#undef ECGF_CASE
-    default:
-#pragma unroll
-        for (int p = 0; p < 8; ++p)
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-                out[p][w] = in[p][w];
-        break;
-    }
-}
-
 } // namespace ecgf
 
 #endif

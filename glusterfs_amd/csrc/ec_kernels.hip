@@ -5,18 +5,24 @@
  * Shipped configuration (tools/kbench A/B runs, profiles/kbench_r01.log):
  *   encode   compile-time Vandermonde rows for 2+1, 4+2, 8+4, 16+4;
  *            W = 4 / 2 / 1 / 1 dwords per plane per lane (VGPR budget)
- *   stores   non-temporal for k > 4 (encode and combine), default for
- *            k <= 4 (profiles/kbench_r01_nts.log).  Without them the
- *            output lines sit dirty in the per-XCD L2 and are written back
- *            at the kernel boundary: 8+4 decode of a 64K-stripe batch
- *            (BASELINE configs[2]) 0.58 -> 0.70 of 8 TB/s, 8+4 encode
- *            0.655 -> 0.670; at k = 4 they cost 3-8 %
- *   combine  one tile per block, staged by LDS-DMA (global_load_lds_dwordx4):
- *            k <= 4: 16-stripe tiles, 4 waves; k > 4: 8-stripe tiles (LDS per
- *            block caps occupancy), 8 waves -- measured (profiles/kbench_r01_*)
- *            8+4 decode 0.57 -> 0.66, 16+4 decode 0.24 -> 0.42, mixed 8+4
- *            0.55 -> 0.63 of 8 TB/s against 4-wave register staging; outputs
- *            are stored straight from registers
+ *   stores   non-temporal for every combine and for the k > 4 encoders;
+ *            default for the 2+1 / 4+2 encoders, where they cost 3-4 %
+ *            (profiles/kbench_r01_nts.log).  Without them the output lines
+ *            sit dirty in the per-XCD L2 and are written back at the kernel
+ *            boundary: 8+4 decode of a 64K-stripe batch (BASELINE
+ *            configs[2]) 0.58 -> 0.70 of 8 TB/s, 8+4 encode 0.655 -> 0.670
+ *   combine  one tile per block, staged by LDS-DMA (global_load_lds_dwordx4)
+ *            into a plane-major tile; outputs stored straight from registers.
+ *            8-stripe tiles; 8 / 4 / 16 waves per block for k <= 4 / 8 / 16
+ *            (5 blocks of 4 waves fit a CU at k = 8; at k = 16 two
+ *            16-wave blocks fill all 32 wave slots, which hides the
+ *            compare-tree dispatch of the multiply).  On the real decode
+ *            matrices (profiles/kbench_r01_combine_cfg.log): 4+2 0.704 ->
+ *            0.722, 8+4 0.656 -> 0.686, 16+4 0.434 -> 0.519 of 8 TB/s.
+ *            History: LDS-DMA over register staging took 8+4 decode
+ *            0.57 -> 0.66 and 16+4 0.24 -> 0.42; the plane-major tile (one
+ *            LDS address per input instead of five) 16+4 0.43 -> 0.45
+ *            (profiles/kbench_r01_combine_pm.log)
  */
 #include <hip/hip_runtime.h>
 
@@ -52,7 +58,7 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-template <int K, int TS, int NW>
+template <int K, int TS, int NW, bool NTS>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     const uint64_t g = combine_grid<TS>(a.nstripes);
@@ -61,13 +67,12 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
     if (g > 0x7fffffffull)
         return -EINVAL;
     const size_t lds = combine_lds<TS>(a.k);
-    constexpr bool NTS = K > 4;
     if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, true, NTS, true>), dim3((u32)g),
-                           dim3(NW * 64), lds, s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, true, NTS>), dim3((u32)g), dim3(NW * 64), lds,
+                           s, a);
     else
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS, true>), dim3((u32)g),
-                           dim3(NW * 64), lds, s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS>), dim3((u32)g), dim3(NW * 64), lds,
+                           s, a);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -180,12 +185,10 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
     int rc = ecdk_pack_args(d, &a);
     if (rc)
         return rc;
-    /* a 16-stripe tile must not straddle two pattern groups */
-    if (d->k <= 4 && (!d->group_pattern || d->group_shift >= 4))
-        return launch_combine<4, 2, 4>(s, a);
+    /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
     if (d->k <= 4)
-        return launch_combine<4, 1, 4>(s, a);
+        return launch_combine<4, 1, 8, true>(s, a);
     if (d->k <= 8)
-        return launch_combine<8, 1, 8>(s, a);
-    return launch_combine<16, 1, 8>(s, a);
+        return launch_combine<8, 1, 4, true>(s, a);
+    return launch_combine<16, 1, 16, true>(s, a);
 }

@@ -16,13 +16,13 @@
  *      A lane owns W dwords of all 8 planes of one chunk column (L = 16/W
  *      lanes per chunk); its k input chunks stay in VGPRs, so HBM is read once.
  *
- *  ec_combine<K, TS, MIXED, NTS>    reference: ec_method_decode
+ *  ec_combine<K, TS, NW, MIXED, NTS>  reference: ec_method_decode
  *      (ec-method.c:411-433) with ec_code_c_interleaved (ec-code-c.c:11660).
  *      Output row r of stripe t = XOR_p coef[r][p] * input_p(t) for a run-time
  *      coefficient matrix held in the kernel-argument segment (constant
  *      memory, scalar loads).  One block = one tile of T = 8*TS stripes: the
- *      k input chunks of the tile are staged through LDS with coalesced
- *      16-byte loads, then each wave computes whole output rows (8 stripes x
+ *      k input chunks of the tile are staged into LDS by LDS-DMA (16 bytes
+ *      per lane, no VGPRs), then each wave computes whole output rows (8 stripes x
  *      8 lanes x 2 dwords per plane) walking the inputs with a run-time index
  *      so a single multiply dispatch serves every coefficient: the
  *      wave-uniform coefficient selects one of 255 compile-time XOR trees
@@ -32,9 +32,14 @@
  * Tuning knobs measured with tools/kbench (profiles/kbench_*.log): one tile
  * per block beats a persistent grid with register prefetch (vmcnt also counts
  * the stores of the previous tile, which serialises the prefetch);
- * non-temporal loads lose; staging the output tile through LDS and a split
- * 16+16-case dispatch measured equal or worse and were removed; NTS
- * (non-temporal stores) and the block size NW remain knobs.
+ * non-temporal loads lose; staging the output tile through LDS, a split
+ * 16+16-case dispatch, register staging, prefetching the next input's LDS
+ * reads, ping-pong accumulators (2 switch copies: i-cache misses x3.6),
+ * 64-bit accumulators (v_mov_b64 join copies: +-10 % depending on the
+ * coefficient matrix), grouped input staging for k = 16 and an explicit
+ * binary compare tree measured equal or worse and were removed; NTS
+ * (non-temporal stores), the tile size TS and the block size NW remain
+ * knobs.
  */
 #ifndef EC_MI355X_KERNELS_IMPL_H
 #define EC_MI355X_KERNELS_IMPL_H
@@ -279,34 +284,26 @@ struct CombineArgs {
     u32 pat[kPatWords];
 };
 
-/* LDS byte offset of 16-byte piece q (0..31) of the chunk of input p, tile
- * stripe s, tile of T stripes.  Plane slots are XOR-rotated by s&3 so the 4
- * stripes a half wave reads with ds_read_b64 hit 4 different 64-byte bank
- * windows (conflict-free), and a ds_write_b128 group of 8 lanes (2 planes of
- * one chunk) covers one full 128-byte bank row. */
-__device__ __forceinline__ u32 lds_piece(u32 p, u32 s, u32 q, u32 T)
-{
-    return (p * T + s) * ECD_CHUNK + ((((q >> 2) ^ (s & 3u)) << 6) | ((q & 3u) << 4));
-}
-
 __device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
 {
     const u32 w = a.pat[word + (idx >> 2)];
     return __builtin_amdgcn_readfirstlane((w >> ((idx & 3u) * 8u)) & 0xFFu);
 }
 
-/* K: max inputs (k <= K); TS: tile = 8*TS stripes; NW: waves per block;
- * GLDS: stage the tile with LDS-DMA (global_load_lds_dwordx4, no VGPRs)
- * instead of global_load + ds_write; PF: issue the next input's LDS reads
- * before each multiply. */
-template <int K, int TS, int NW, bool MIXED, bool NTS, bool GLDS = false, bool PF = false,
-          bool PP = false>
+/* K: max inputs (k <= K); TS: tile = 8*TS stripes; NW: waves per block.
+ *
+ * LDS tile, plane-major: input p, plane b, tile stripe s, 64-byte segment at
+ * ((p * 8 + b) * T + s) * 64.  The half wave that reads plane b of 4 stripes
+ * with ds_read_b64 then touches 256 consecutive bytes (conflict-free), and
+ * one lane address serves all 8 planes of an input (ds_read2st64_b64 with
+ * immediate plane offsets) -- the earlier chunk-major tile needed an
+ * XOR-rotated plane slot, hence 5 address VALUs per input. */
+template <int K, int TS, int NW, bool MIXED, bool NTS>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
-    constexpr u32 NT = NW * 64;          /* threads per block                  */
-    constexpr u32 PER = (K * T * 32 + NT - 1) / NT; /* staged pieces per thread */
     constexpr int CW = 2;                /* dwords per plane per lane (compute) */
+    constexpr u32 NI = K * T * 32 / 64;  /* LDS-DMA wave instructions per tile */
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
     const u32 k = a.k;
@@ -318,52 +315,28 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     if constexpr (MIXED)
         pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
 
-    if constexpr (GLDS) {
-        /* every wave instruction fills 1 KiB of LDS linearly (2 chunks of one
-         * input); the XOR plane rotation is applied to the per-lane source
-         * address instead of the destination */
-        constexpr u32 NI = K * T * 32 / 64; /* wave instructions per tile */
+    /* stage: every wave instruction (global_load_lds_dwordx4) fills 1 KiB of
+     * LDS linearly = planes b, b+1 of input p for the tile's 8 stripes (T=8)
+     * or plane b for 16 (T=16); lane i fetches 16-byte piece i, so the tile
+     * layout above is produced by the per-lane source address alone */
 #pragma unroll
-        for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
-            const u32 ins = j * NW + wave;           /* wave-uniform */
-            if (ins >= NI)
-                break;
-            const u32 p = ins / (T / 2);
-            if (p >= k)
-                break;
-            const u32 e = ins * 64 + lane;            /* LDS piece */
-            const u32 s = (e / 32) % T, slot = e & 31u;
-            const uint64_t st = t0 + s;
-            if (st < a.nstripes) {
-                const u32 src = pat_byte(a, pb, p);
-                const uint8_t *g = a.in_base[src] + st * a.in_stride +
-                                   ((((slot >> 2) ^ (s & 3u)) << 6) | ((slot & 3u) << 4));
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)g,
-                    (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
-            }
-        }
-    } else {
-        /* stage: 16-byte pieces e = (input p, stripe s, piece q), coalesced */
-        uint4 v[PER];
-#pragma unroll
-        for (u32 j = 0; j < PER; ++j) {
-            const u32 e = tid + j * NT;
-            const u32 p = e / (T * 32), s = (e / 32) % T, q = e & 31u;
-            const uint64_t st = t0 + s;
-            v[j] = make_uint4(0, 0, 0, 0);
-            if (p < k && st < a.nstripes) {
-                const u32 src = pat_byte(a, pb, p);
-                v[j] = *reinterpret_cast<const uint4 *>(a.in_base[src] + st * a.in_stride +
-                                                        q * 16u);
-            }
-        }
-#pragma unroll
-        for (u32 j = 0; j < PER; ++j) {
-            const u32 e = tid + j * NT;
-            const u32 p = e / (T * 32), s = (e / 32) % T, q = e & 31u;
-            if (p < k)
-                *reinterpret_cast<uint4 *>(lds + lds_piece(p, s, q, T)) = v[j];
+    for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
+        const u32 ins = j * NW + wave;           /* wave-uniform */
+        if (ins >= NI)
+            break;
+        const u32 p = ins / (T / 2);
+        if (p >= k)
+            break;
+        const u32 el = (ins * 64 + lane) % (T * 32); /* piece within input p */
+        const u32 s = (el >> 2) % T;
+        const uint64_t st = t0 + s;
+        if (st < a.nstripes) {
+            const u32 src = pat_byte(a, pb, p);
+            const uint8_t *g = a.in_base[src] + st * a.in_stride + ((el >> 2) / T) * 64u +
+                               (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
         }
     }
     __syncthreads();
@@ -373,8 +346,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     const u32 items = a.rows * TS;
     for (u32 it = wave; it < items; it += NW) {
         const u32 r = it / TS, s = (it % TS) * 8u + cs;
-        const u32 rot = (s & 3u) << 6;
-        const uint8_t *col = lds + s * ECD_CHUNK + cc * 8u;
+        const uint8_t *col = lds + s * 64u + cc * 8u;
         /* the row's coefficients: up to 4 words, loaded once into SGPRs */
         const u32 rw = pb + a.kw * (1 + r);
         const u32 w0 = a.pat[rw];
@@ -384,162 +356,24 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         u32 acc[8][CW], y[8][CW];
 #pragma unroll
         for (int b = 0; b < 8; ++b)
-#pragma unroll
-            for (int w = 0; w < CW; ++w)
-                acc[b][w] = 0;
-        auto read_input = [&](u32 p, u32 (&d)[8][CW]) {
+            acc[b][0] = acc[b][1] = 0;
+        for (u32 p = 0; p < k; ++p) {
+            const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
+            const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
+            if (c == 0)                  /* ec-code-c.c:11666-11676 */
+                continue;
             const uint8_t *src = col + p * (T * ECD_CHUNK);
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
-                const uint2 t = *reinterpret_cast<const uint2 *>(src + (((u32)b << 6) ^ rot));
-                d[b][0] = t.x;
-                d[b][1] = t.y;
+                const uint2 t = *reinterpret_cast<const uint2 *>(src + (u32)b * (T * 64u));
+                y[b][0] = t.x;
+                y[b][1] = t.y;
             }
-        };
-        auto coef = [&](u32 p) {
-            const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
-            return __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
-        };
-        if constexpr (PP) {
-            /* ping-pong accumulators (ecgf::mul_xor_rt_pp): acc -> y2 -> acc */
-            u32 acc2[8][CW];
-            for (u32 p = 0; p < k; p += 2) {
-                const u32 c0 = coef(p);
-                if (c0)
-                    read_input(p, y);
-                ecgf::mul_xor_rt_pp<CW>(c0, acc, acc2, y);
-                const u32 c1 = p + 1 < k ? coef(p + 1) : 0u;
-                if (c1)
-                    read_input(p + 1, y);
-                ecgf::mul_xor_rt_pp<CW>(c1, acc2, acc, y);
-            }
-        } else {
-            if constexpr (PF)
-                read_input(0, y);
-            for (u32 p = 0; p < k; ++p) {
-                const u32 c = coef(p);
-                if constexpr (PF) {
-                    /* issue the next input's LDS reads before this multiply */
-                    u32 yn[8][CW];
-                    read_input(p + 1 < k ? p + 1 : p, yn);
-                    ecgf::mul_xor_rt<CW>(c, acc, y);
-#pragma unroll
-                    for (int b = 0; b < 8; ++b)
-#pragma unroll
-                        for (int w = 0; w < CW; ++w)
-                            y[b][w] = yn[b][w];
-                } else {
-                    if (c == 0)
-                        continue;
-                    read_input(p, y);
-                    ecgf::mul_xor_rt<CW>(c, acc, y);
-                }
-            }
+            ecgf::mul_xor_rt<CW>(c, acc, y);
         }
         const uint64_t ost = t0 + s;
         if (ost < a.nstripes)
             store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
-    }
-}
-
-/* ec_combine for wide codes (k > G): the tile's inputs are staged and
- * consumed in groups of G fragments through one G-input LDS buffer, the
- * output rows accumulating in VGPRs across groups (wave w owns items w,
- * w + NW, ...; at most IPW each).  LDS per block drops from k to G inputs,
- * so more blocks share a CU and one block's XOR-heavy compute phase overlaps
- * other blocks' loads and stores -- at k = 16 the single-phase kernel holds
- * 2 blocks per CU and runs its memory and VALU phases nearly back to back. */
-template <int K, int G, int NW, int IPW, bool MIXED, bool NTS>
-__global__ __launch_bounds__(NW * 64) void ec_combine_grouped(const CombineArgs a)
-{
-    constexpr u32 T = 8;                 /* stripes per tile                   */
-    constexpr int CW = 2;
-    constexpr u32 NI = G * T * 32 / 64;  /* LDS-DMA wave instructions / group */
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const u32 tid = threadIdx.x;
-    const u32 k = a.k;
-    const uint64_t t0 = (uint64_t)blockIdx.x * T;
-    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const u32 lane = tid & 63u;
-    const u32 cs = lane >> 3, cc = lane & 7u;
-    const u32 rot = (cs & 3u) << 6;
-    const uint8_t *col = lds + cs * ECD_CHUNK + cc * 8u;
-
-    u32 pb = 0;
-    if constexpr (MIXED)
-        pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
-
-    u32 acc[IPW][8][CW];
-#pragma unroll
-    for (int j = 0; j < IPW; ++j)
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-#pragma unroll
-            for (int w = 0; w < CW; ++w)
-                acc[j][b][w] = 0;
-
-    for (u32 g0 = 0; g0 < k; g0 += G) {
-        if (g0)
-            __syncthreads();             /* everyone is done with the buffer */
-#pragma unroll
-        for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
-            const u32 ins = j * NW + wave;
-            if (ins >= NI)
-                break;
-            const u32 p = g0 + ins / (T / 2);
-            if (p >= k)
-                break;
-            const u32 e = ins * 64 + lane;
-            const u32 s = (e / 32) % T, slot = e & 31u;
-            const uint64_t st = t0 + s;
-            if (st < a.nstripes) {
-                const u32 src = pat_byte(a, pb, p);
-                const uint8_t *gp = a.in_base[src] + st * a.in_stride +
-                                    ((((slot >> 2) ^ (s & 3u)) << 6) | ((slot & 3u) << 4));
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)gp,
-                    (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
-            }
-        }
-        __syncthreads();
-        const u32 ng = k - g0 < (u32)G ? k - g0 : (u32)G;
-        /* the items' coefficient words for this group (<= 2 words each) */
-        u32 cw[IPW][2];
-        static_for<0, IPW>([&](auto jj) {
-            constexpr int j = decltype(jj)::value;
-            const u32 r = wave + (u32)j * NW;
-            const u32 rw = pb + a.kw * (1 + (r < a.rows ? r : 0)) + (g0 >> 2);
-            cw[j][0] = a.pat[rw];
-            cw[j][1] = G > 4 ? a.pat[rw + 1] : 0u;
-        });
-        for (u32 q = 0; q < ng; ++q) {
-            /* one LDS read of input q serves all of this wave's rows */
-            u32 y[8][CW];
-            const uint8_t *src = col + q * (T * ECD_CHUNK);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const uint2 t = *reinterpret_cast<const uint2 *>(src + (((u32)b << 6) ^ rot));
-                y[b][0] = t.x;
-                y[b][1] = t.y;
-            }
-            static_for<0, IPW>([&](auto jj) {
-                constexpr int j = decltype(jj)::value;
-                const u32 wsel = q < 4 ? cw[j][0] : cw[j][1];
-                u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((q & 3u) * 8u)) & 0xFFu);
-                if (wave + (u32)j * NW >= a.rows)
-                    c = 0;
-                ecgf::mul_xor_rt<CW>(c, acc[j], y);
-            });
-        }
-    }
-    const uint64_t ost = t0 + cs;
-    if (ost < a.nstripes) {
-        static_for<0, IPW>([&](auto jj) {
-            constexpr int j = decltype(jj)::value;
-            const u32 r = wave + (u32)j * NW;
-            if (r < a.rows)
-                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc[j]);
-        });
     }
 }
 

@@ -196,18 +196,14 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
                             hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * nw), lds, s, a);
                         }, out, ob});
     };
+    /* (GLDS / PF / register staging were measured here in r01a-c and
+     * removed; the shipped kernel stages by LDS-DMA into a plane-major tile) */
     add("TS1 NW4", ec_combine<K, 1, 4, false, false>, 1, 4);
-    add("TS1 NW4 GLDS", ec_combine<K, 1, 4, false, false, true>, 1, 4);
-    add("TS1 NW4 GLDS PF", ec_combine<K, 1, 4, false, false, true, true>, 1, 4);
     add("TS1 NW8", ec_combine<K, 1, 8, false, false>, 1, 8);
-    add("TS1 NW8 GLDS", ec_combine<K, 1, 8, false, false, true>, 1, 8);
-    add("TS1 NW8 GLDS PF", ec_combine<K, 1, 8, false, false, true, true>, 1, 8);
+    add("TS1 NW8 NTS", ec_combine<K, 1, 8, false, true>, 1, 8);
     if (K <= 4) {
         add("TS2 NW4", ec_combine<K, 2, 4, false, false>, 2, 4);
-        add("TS2 NW4 GLDS", ec_combine<K, 2, 4, false, false, true>, 2, 4);
         add("TS2 NW8", ec_combine<K, 2, 8, false, false>, 2, 8);
-        add("TS2 NW8 GLDS", ec_combine<K, 2, 8, false, false, true>, 2, 8);
-        add("TS2 NW8 GLDS PF", ec_combine<K, 2, 8, false, false, true, true>, 2, 8);
     }
 }
 
@@ -354,16 +350,16 @@ int main(int argc, char **argv)
         std::vector<Variant> v;
         const size_t lds = (size_t)K * 8 * ECD_CHUNK;
         const uint64_t g = (nst + 7) / 8;
-        v.push_back({"mixed TS1 NW4", bytes, [=](hipStream_t st) {
-                         hipLaunchKernelGGL((ec_combine<K, 1, 4, true, false>), dim3((u32)g),
+        v.push_back({"mixed TS1 NW4 NTS", bytes, [=](hipStream_t st) {
+                         hipLaunchKernelGGL((ec_combine<K, 1, 4, true, true>), dim3((u32)g),
                                             dim3(256), lds, st, a);
                      }, bufB, (size_t)nst * K * ECD_CHUNK});
-        v.push_back({"mixed TS1 NW8 GLDS", bytes, [=](hipStream_t st) {
-                         hipLaunchKernelGGL((ec_combine<K, 1, 8, true, false, true>), dim3((u32)g),
+        v.push_back({"mixed TS1 NW8 NTS", bytes, [=](hipStream_t st) {
+                         hipLaunchKernelGGL((ec_combine<K, 1, 8, true, true>), dim3((u32)g),
                                             dim3(512), lds, st, a);
                      }, bufB, (size_t)nst * K * ECD_CHUNK});
-        v.push_back({"mixed TS1 NW8 GLDS PF", bytes, [=](hipStream_t st) {
-                         hipLaunchKernelGGL((ec_combine<K, 1, 8, true, false, true, true>),
+        v.push_back({"mixed TS1 NW8", bytes, [=](hipStream_t st) {
+                         hipLaunchKernelGGL((ec_combine<K, 1, 8, true, false>),
                                             dim3((u32)g), dim3(512), lds, st, a);
                      }, bufB, (size_t)nst * K * ECD_CHUNK});
         run_group("decode 8+4 mixed (16 patterns, 1024-stripe groups)", v, rounds, iters, s);

@@ -245,7 +245,7 @@ int main(int argc, char **argv)
         std::vector<Variant> v;
         v.push_back({"combine TS2 NW4 GLDS (shipped)", bytes, [=](hipStream_t st) {
                          const size_t lds = (size_t)K * 8 * 2 * ECD_CHUNK;
-                         hipLaunchKernelGGL((ec_combine<4, 2, 4, false, false, true>),
+                         hipLaunchKernelGGL((ec_combine<4, 2, 4, false, false>),
                                             dim3((u32)((nst + 15) / 16)), dim3(256), lds, st, a);
                      }, bufB, ob});
         auto addst = [&](const char *nm, auto kern, int W) {
@@ -322,14 +322,14 @@ int main(int argc, char **argv)
                              }, bufB, (size_t)nst * K * ECD_CHUNK});
             };
             if (K == 4) {
-                addd("dec TS2 NW4", ec_combine<4, 2, 4, false, false, true>, 2, 4);
-                addd("dec TS2 NW4 NTS", ec_combine<4, 2, 4, false, true, true>, 2, 4);
+                addd("dec TS2 NW4", ec_combine<4, 2, 4, false, false>, 2, 4);
+                addd("dec TS2 NW4 NTS", ec_combine<4, 2, 4, false, true>, 2, 4);
             } else if (K == 8) {
-                addd("dec NW8", ec_combine<8, 1, 8, false, false, true>, 1, 8);
-                addd("dec NW8 NTS", ec_combine<8, 1, 8, false, true, true>, 1, 8);
+                addd("dec NW8", ec_combine<8, 1, 8, false, false>, 1, 8);
+                addd("dec NW8 NTS", ec_combine<8, 1, 8, false, true>, 1, 8);
             } else {
-                addd("dec NW8", ec_combine<16, 1, 8, false, false, true>, 1, 8);
-                addd("dec NW8 NTS", ec_combine<16, 1, 8, false, true, true>, 1, 8);
+                addd("dec NW8", ec_combine<16, 1, 8, false, false>, 1, 8);
+                addd("dec NW8 NTS", ec_combine<16, 1, 8, false, true>, 1, 8);
             }
             snprintf(title, sizeof title, "decode %d+%d dense, %lu stripes", K, N - K,
                      (unsigned long)nst);
@@ -337,11 +337,15 @@ int main(int argc, char **argv)
         }
     }
     }
-    /* D) tied in-place multiply (no phi copies) */
+    /* D) combine variants (tile, block size, NT stores) on the real decode
+     * matrices of 4+2 mask 0x3C, 8+4 0xFF0 and 16+4 0xFFFF0 */
     for (const int K : {4, 8, 16}) {
         if (getenv("KB_K") && atoi(getenv("KB_K")) != K)
             continue;
         const uint64_t nst = (uint64_t)(gib * (1ull << 30)) / (K * ECD_CHUNK);
+        const proto::Mat M = K == 4   ? proto::decode_matrix<4, 0x3C>()
+                             : K == 8 ? proto::decode_matrix<8, 0xFF0>()
+                                      : proto::decode_matrix<16, 0xFFFF0>();
         ecd_combine_desc_t d;
         memset(&d, 0, sizeof(d));
         d.k = K;
@@ -353,10 +357,11 @@ int main(int argc, char **argv)
             d.in_base[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
             d.pat[p] = (uint8_t)p;
         }
-        for (int r = 0; r < K; ++r)
+        for (int r = 0; r < K; ++r) {
             d.out_base[r] = bufB + (uint64_t)r * ECD_CHUNK;
-        for (int i = 0; i < K * K; ++i)
-            d.pat[K + i] = (uint8_t)(1 + (i * 173 + 11) % 255);
+            for (int p = 0; p < K; ++p)
+                d.pat[K + r * K + p] = (uint8_t)M.m[r][p];
+        }
         d.npatterns = 1;
         d.pat_bytes = K + K * K;
         static CombineArgs a;
@@ -371,69 +376,24 @@ int main(int argc, char **argv)
                          }, bufB, (size_t)nst * K * ECD_CHUNK});
         };
         if (K == 4) {
-            addd("TS2 NW4 (shipped)", ec_combine<4, 2, 4, false, false, true>, 2, 4);
-            addd("TS2 NW4 PP", ec_combine<4, 2, 4, false, false, true, false, true>, 2, 4);
+            addd("TS2 NW4 (shipped)", ec_combine<4, 2, 4, false, false>, 2, 4);
+            addd("TS2 NW4 NTS", ec_combine<4, 2, 4, false, true>, 2, 4);
+            addd("TS2 NW8 NTS", ec_combine<4, 2, 8, false, true>, 2, 8);
+            addd("TS1 NW8", ec_combine<4, 1, 8, false, false>, 1, 8);
+            addd("TS1 NW8 NTS", ec_combine<4, 1, 8, false, true>, 1, 8);
         } else if (K == 8) {
-            addd("NW8 NTS (shipped)", ec_combine<8, 1, 8, false, true, true>, 1, 8);
-            addd("NW8 NTS PP", ec_combine<8, 1, 8, false, true, true, false, true>, 1, 8);
+            addd("NW8 NTS (shipped)", ec_combine<8, 1, 8, false, true>, 1, 8);
+            addd("NW8", ec_combine<8, 1, 8, false, false>, 1, 8);
+            addd("NW4 NTS", ec_combine<8, 1, 4, false, true>, 1, 4);
+            addd("NW16 NTS", ec_combine<8, 1, 16, false, true>, 1, 16);
         } else {
-            addd("NW8 NTS (shipped)", ec_combine<16, 1, 8, false, true, true>, 1, 8);
-            addd("NW8 NTS PP", ec_combine<16, 1, 8, false, true, true, false, true>, 1, 8);
+            addd("NW8 NTS (shipped)", ec_combine<16, 1, 8, false, true>, 1, 8);
+            addd("NW16 NTS", ec_combine<16, 1, 16, false, true>, 1, 16);
+            addd("NW16", ec_combine<16, 1, 16, false, false>, 1, 16);
         }
         char title[96];
-        snprintf(title, sizeof title, "decode %d dense (PP), %lu stripes", K, (unsigned long)nst);
-        run_group(title, v, rounds, iters, s);
-    }
-    if (getenv("KB_GROUPED"))
-    for (const int K : {8, 16, 160}) {
-        /* K = 160: 16+4 with coefficients from only 16 distinct values */
-        const bool few = K == 160;
-        const int KK = few ? 16 : K;
-        const uint64_t nst = (uint64_t)(gib * (1ull << 30)) / (KK * ECD_CHUNK);
-        ecd_combine_desc_t d;
-        memset(&d, 0, sizeof(d));
-        d.k = KK;
-        d.rows = KK;
-        d.nstripes = nst;
-        d.in_stride = ECD_CHUNK;
-        d.out_stride = (uint64_t)KK * ECD_CHUNK;
-        for (int p = 0; p < KK; ++p) {
-            d.in_base[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
-            d.pat[p] = (uint8_t)p;
-        }
-        for (int r = 0; r < KK; ++r)
-            d.out_base[r] = bufB + (uint64_t)r * ECD_CHUNK;
-        for (int i = 0; i < KK * KK; ++i)
-            d.pat[KK + i] = (uint8_t)(1 + ((few ? i % 16 : i) * 173 + 11) % 255);
-        d.npatterns = 1;
-        d.pat_bytes = KK + KK * KK;
-        static CombineArgs a;
-        if (ecdk_pack_args(&d, &a))
-            exit(2);
-        const double db = 2.0 * nst * KK * ECD_CHUNK;
-        std::vector<Variant> v;
-        auto addd = [&](const char *nm, auto kern, int nw, size_t lds) {
-            v.push_back({nm, db, [=](hipStream_t st) {
-                             hipLaunchKernelGGL(kern, dim3((u32)(nst / 8)), dim3(64 * nw), lds,
-                                                st, a);
-                         }, bufB, (size_t)nst * KK * ECD_CHUNK});
-        };
-        if (KK == 16) {
-            addd("single-phase NW8 NTS (shipped)", ec_combine<16, 1, 8, false, true, true>, 8,
-                 16 * 4096);
-            addd("grouped G8 NW8 NTS", ec_combine_grouped<16, 8, 8, 2, false, true>, 8, 8 * 4096);
-            addd("grouped G4 NW8 NTS", ec_combine_grouped<16, 4, 8, 2, false, true>, 8, 4 * 4096);
-            addd("grouped G8 NW4 NTS", ec_combine_grouped<16, 8, 4, 4, false, true>, 4, 8 * 4096);
-            addd("grouped G4 NW4 NTS", ec_combine_grouped<16, 4, 4, 4, false, true>, 4, 4 * 4096);
-        } else {
-            addd("single-phase NW8 NTS (shipped)", ec_combine<8, 1, 8, false, true, true>, 8,
-                 8 * 4096);
-            addd("grouped G4 NW8 NTS", ec_combine_grouped<8, 4, 8, 1, false, true>, 8, 4 * 4096);
-            addd("grouped G8 NW4 NTS", ec_combine_grouped<8, 8, 4, 2, false, true>, 4, 8 * 4096);
-            addd("grouped G4 NW4 NTS", ec_combine_grouped<8, 4, 4, 2, false, true>, 4, 4 * 4096);
-        }
-        char title[96];
-        snprintf(title, sizeof title, "decode %d dense, %lu stripes", K, (unsigned long)nst);
+        snprintf(title, sizeof title, "decode %d+%d real inverse, %lu stripes", K,
+                 K == 16 ? 4 : K / 2, (unsigned long)nst);
         run_group(title, v, rounds, iters, s);
     }
     return 0;
