@@ -14,11 +14,12 @@
  *   combine  one tile per block, staged by LDS-DMA (global_load_lds_dwordx4)
  *            into a plane-major tile; outputs stored straight from registers.
  *            8-stripe tiles; 8 / 4 / 16 waves per block for k <= 4 / 8 / 16
- *            (5 blocks of 4 waves fit a CU at k = 8; at k = 16 two
- *            16-wave blocks fill all 32 wave slots, which hides the
- *            compare-tree dispatch of the multiply).  On the real decode
- *            matrices (profiles/kbench_r01_combine_cfg.log): 4+2 0.704 ->
- *            0.722, 8+4 0.656 -> 0.686, 16+4 0.434 -> 0.519 of 8 TB/s.
+ *            (8 waves for 8+4 mixed patterns).  At k = 16 two 16-wave
+ *            blocks fill all 32 wave slots of a CU, which hides the
+ *            compare-tree dispatch of the multiply.  Two back-to-back
+ *            processes, 21 interleaved rounds (profiles/kbench_r01_nw*.log):
+ *            4+2 0x3C 0.707 -> 0.725-0.736, 8+4 dense 0.665 -> 0.669-0.676,
+ *            8+4 mixed 0.651-0.673, 16+4 0.43 -> 0.506 of 8 TB/s.
  *            History: LDS-DMA over register staging took 8+4 decode
  *            0.57 -> 0.66 and 16+4 0.24 -> 0.42; the plane-major tile (one
  *            LDS address per input instead of five) 16+4 0.43 -> 0.45
@@ -58,7 +59,8 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-template <int K, int TS, int NW, bool NTS>
+/* NW: waves per block for a single pattern; NWM: for mixed patterns */
+template <int K, int TS, int NW, int NWM, bool NTS>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     const uint64_t g = combine_grid<TS>(a.nstripes);
@@ -68,8 +70,8 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
         return -EINVAL;
     const size_t lds = combine_lds<TS>(a.k);
     if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, true, NTS>), dim3((u32)g), dim3(NW * 64), lds,
-                           s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS>), dim3((u32)g), dim3(NWM * 64),
+                           lds, s, a);
     else
         hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS>), dim3((u32)g), dim3(NW * 64), lds,
                            s, a);
@@ -187,8 +189,8 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
         return rc;
     /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
     if (d->k <= 4)
-        return launch_combine<4, 1, 8, true>(s, a);
+        return launch_combine<4, 1, 8, 8, true>(s, a);
     if (d->k <= 8)
-        return launch_combine<8, 1, 4, true>(s, a);
-    return launch_combine<16, 1, 16, true>(s, a);
+        return launch_combine<8, 1, 4, 8, true>(s, a);
+    return launch_combine<16, 1, 16, 16, true>(s, a);
 }

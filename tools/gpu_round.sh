@@ -19,6 +19,6 @@ step bench_2rank_rehearsal 600 env EC_BENCH_BACKEND=gloo EC_BENCH_DEVICE=0 \
   --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1
 step bench 900 python bench.py
 if [ "${PROFILE:-1}" = 1 ]; then
-  step profile 900 bash tools/profile.sh ${TAG:-r01b} dec:4+2:3C 1 enc:4+2 1 enc:8+4 0.25 \
-    dec:8+4:FF0 0.25 enc:16+4 2 mixed:8+4 1 heal:8+4 1
+  step profile 1000 bash tools/profile.sh ${TAG:-r01d} dec:4+2:3C 1 enc:4+2 1 enc:8+4 0.25 \
+    dec:8+4:FF0 0.25 enc:16+4 2 mixed:8+4 1 heal:8+4 1 dec:16+4:FFFF0 1
 fi

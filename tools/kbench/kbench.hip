@@ -198,13 +198,13 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     };
     /* (GLDS / PF / register staging were measured here in r01a-c and
      * removed; the shipped kernel stages by LDS-DMA into a plane-major tile) */
+    add("TS1 NW4 NTS", ec_combine<K, 1, 4, false, true>, 1, 4);
+    add("TS1 NW8 NTS", ec_combine<K, 1, 8, false, true>, 1, 8);
+    add("TS1 NW16 NTS", ec_combine<K, 1, 16, false, true>, 1, 16);
+    if (K <= 4)
+        add("TS2 NW4", ec_combine<K, 2, 4, false, false>, 2, 4);
     add("TS1 NW4", ec_combine<K, 1, 4, false, false>, 1, 4);
     add("TS1 NW8", ec_combine<K, 1, 8, false, false>, 1, 8);
-    add("TS1 NW8 NTS", ec_combine<K, 1, 8, false, true>, 1, 8);
-    if (K <= 4) {
-        add("TS2 NW4", ec_combine<K, 2, 4, false, false>, 2, 4);
-        add("TS2 NW8", ec_combine<K, 2, 8, false, false>, 2, 8);
-    }
 }
 
 template <int K, int N, typename KF>
@@ -350,18 +350,14 @@ int main(int argc, char **argv)
         std::vector<Variant> v;
         const size_t lds = (size_t)K * 8 * ECD_CHUNK;
         const uint64_t g = (nst + 7) / 8;
-        v.push_back({"mixed TS1 NW4 NTS", bytes, [=](hipStream_t st) {
-                         hipLaunchKernelGGL((ec_combine<K, 1, 4, true, true>), dim3((u32)g),
-                                            dim3(256), lds, st, a);
-                     }, bufB, (size_t)nst * K * ECD_CHUNK});
-        v.push_back({"mixed TS1 NW8 NTS", bytes, [=](hipStream_t st) {
-                         hipLaunchKernelGGL((ec_combine<K, 1, 8, true, true>), dim3((u32)g),
-                                            dim3(512), lds, st, a);
-                     }, bufB, (size_t)nst * K * ECD_CHUNK});
-        v.push_back({"mixed TS1 NW8", bytes, [=](hipStream_t st) {
-                         hipLaunchKernelGGL((ec_combine<K, 1, 8, true, false>),
-                                            dim3((u32)g), dim3(512), lds, st, a);
-                     }, bufB, (size_t)nst * K * ECD_CHUNK});
+        auto addm = [&](const char *nm, auto kern, int nw) {
+            v.push_back({nm, bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * nw), lds, st, a);
+                         }, bufB, (size_t)nst * K * ECD_CHUNK});
+        };
+        addm("mixed TS1 NW4 NTS", ec_combine<K, 1, 4, true, true>, 4);
+        addm("mixed TS1 NW8 NTS", ec_combine<K, 1, 8, true, true>, 8);
+        addm("mixed TS1 NW16 NTS", ec_combine<K, 1, 16, true, true>, 16);
         run_group("decode 8+4 mixed (16 patterns, 1024-stripe groups)", v, rounds, iters, s);
     }
     if (getenv("KB_ENCODE")) {   /* encode 4+2, 8+4, 16+4 */

@@ -63,7 +63,8 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     traffic_path = sys.argv[3] if len(sys.argv) > 3 else None
     gib = {"dec_4p2_3C": 1, "enc_4p2": 1, "enc_8p4": 0.25, "dec_8p4_FF0": 0.25,
-           "enc_16p4": 2, "dec_8p4_EB5": 0.25, "dec_4p2_0F": 1, "mixed_8p4": 1, "heal_8p4": 1}
+           "enc_16p4": 2, "dec_8p4_EB5": 0.25, "dec_4p2_0F": 1, "mixed_8p4": 1, "heal_8p4": 1,
+           "dec_16p4_FFFF0": 1}
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     lines = ["# rocprofv3 summary (%s)" % os.path.basename(src.rstrip("/")), "",
              "| config | kernel | calls | avg us | user GB/s | algorithmic GB/s | HBM frac "
