@@ -224,31 +224,16 @@ or_prepare(uint32_t *values, uint32_t count)
 /* ---------------------------------------------------------- chunk kernels */
 
 /* ec-code-c.c:20-11571 semantics: out = out * c ^ in over one 512-B chunk of
- * 8 bit-planes x 8 u64 words.  c == 0 is the reference's memcpy (:19-23). */
-static void
+ * 8 bit-planes x 8 u64 words.  c == 0 is the reference's memcpy (:19-23).
+ * The per-constant straight-line bodies are generated from the 8x8 GF(2)
+ * matrix of c (oracle/gen_muladd.py -> or_muladd_gen.h), like the
+ * reference's own 256 gf8_muladd_XX routines. */
+#include "or_muladd_gen.h"
+
+static inline void
 or_muladd_i(void *out, const void *in, uint32_t c)
 {
-    uint64_t *o = (uint64_t *)out;
-    const uint64_t *x = (const uint64_t *)in;
-    uint64_t src[8][OR_WIDTH];
-    uint64_t res[OR_WIDTH];
-    uint32_t p, b, w;
-    uint8_t m;
-
-    memcpy(src, o, sizeof(src));
-    for (p = 0; p < 8; p++) {
-        for (w = 0; w < OR_WIDTH; w++)
-            res[w] = x[p * OR_WIDTH + w];
-        m = or_rowmask[c & 0xff][p];
-        for (b = 0; b < 8; b++) {
-            if (m & (1u << b)) {
-                for (w = 0; w < OR_WIDTH; w++)
-                    res[w] ^= src[b][w];
-            }
-        }
-        for (w = 0; w < OR_WIDTH; w++)
-            o[p * OR_WIDTH + w] = res[w];
-    }
+    or_mx[c & 0xff]((uint64_t *)out, (const uint64_t *)in);
 }
 
 void

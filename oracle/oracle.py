@@ -110,11 +110,17 @@ def fill_xorshift(size, seed=SEED):
     return buf
 
 
-def encode(k, n, data, nthreads=1):
-    """data: uint8 array, size multiple of 512*k -> list of n fragments."""
+def encode(k, n, data, nthreads=1, out=None):
+    """data: uint8 array, size multiple of 512*k -> list of n fragments
+    (written into `out`, n preallocated arrays of size/k bytes, if given)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     fsize = data.size // k
-    frags = [np.empty(fsize, dtype=np.uint8) for _ in range(n)]
+    if out is None:
+        frags = [np.empty(fsize, dtype=np.uint8) for _ in range(n)]
+    else:
+        frags = list(out)
+        assert len(frags) == n and all(f.size == fsize and f.dtype == np.uint8 and
+                                       f.flags.c_contiguous for f in frags)
     ptrs = (ctypes.c_void_p * n)(*[f.ctypes.data for f in frags])
     if nthreads > 1:
         rc = lib().or_encode_mt(k, n, data.size, _ptr(data), ptrs, nthreads)
@@ -125,12 +131,15 @@ def encode(k, n, data, nthreads=1):
     return frags
 
 
-def decode(k, rows, frags, nthreads=1):
-    """rows: brick_idx+1 ascending (len k); frags: the k matching fragments."""
+def decode(k, rows, frags, nthreads=1, out=None):
+    """rows: brick_idx+1 ascending (len k); frags: the k matching fragments.
+    Returns the decoded data (written into `out`, size*k bytes, if given)."""
     rows = np.ascontiguousarray(rows, dtype=np.uint32)
     frags = [np.ascontiguousarray(f, dtype=np.uint8) for f in frags]
     size = frags[0].size
-    out = np.empty(size * k, dtype=np.uint8)
+    if out is None:
+        out = np.empty(size * k, dtype=np.uint8)
+    assert out.size == size * k and out.dtype == np.uint8 and out.flags.c_contiguous
     ptrs = (ctypes.c_void_p * k)(*[f.ctypes.data for f in frags])
     if nthreads > 1:
         rc = lib().or_decode_mt(k, size, _ptr(rows), ptrs, _ptr(out), nthreads)

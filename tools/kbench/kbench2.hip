@@ -88,7 +88,7 @@ struct InPtrs {
     const uint8_t *p[16];
 };
 
-template <int K, uint32_t MASK, int W, int R>
+template <int K, uint32_t MASK, int W, int R, bool NTS = false>
 __device__ __forceinline__ void decode_row(const u32 (&x)[K][8][W], uint8_t *dst)
 {
     constexpr Mat M = decode_matrix<K, MASK>();
@@ -103,10 +103,10 @@ __device__ __forceinline__ void decode_row(const u32 (&x)[K][8][W], uint8_t *dst
         if constexpr (c != 0)
             ecgf::mul_xor<c, W>(acc, acc, x[decltype(p)::value]);
     });
-    store_chunk<W, false>(dst, acc);
+    store_chunk<W, NTS>(dst, acc);
 }
 
-template <int K, uint32_t MASK, int W>
+template <int K, uint32_t MASK, int W, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void ec_decode_static(const InPtrs in, uint8_t *out,
                                                            uint64_t nstripes)
 {
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(kBlock) void ec_decode_static(const InPtrs in, uint
         load_chunk<W>(in.p[p] + stripe * (uint64_t)ECD_CHUNK + colb, x[p]);
     uint8_t *o = out + stripe * (uint64_t)(K * ECD_CHUNK) + colb;
     static_for<0, K>([&](auto r) {
-        decode_row<K, MASK, W, decltype(r)::value>(x, o + decltype(r)::value * ECD_CHUNK);
+        decode_row<K, MASK, W, decltype(r)::value, NTS>(x, o + decltype(r)::value * ECD_CHUNK);
     });
 }
 
@@ -194,22 +194,10 @@ static void run_group(const char *title, std::vector<Variant> &vars, int rounds,
     fflush(stdout);
 }
 
-int main(int argc, char **argv)
+template <int K, uint32_t MASK>
+static void static_group(uint8_t *bufA, uint8_t *bufB, uint64_t user, int rounds, int iters,
+                         hipStream_t s)
 {
-    const double gib = argc > 1 ? atof(argv[1]) : 1.0;
-    const int rounds = argc > 2 ? atoi(argv[2]) : 7;
-    const int iters = 10;
-    hipStream_t s;
-    CHK(hipStreamCreate(&s));
-    const uint64_t user = (uint64_t)(gib * (1ull << 30));
-    uint8_t *bufA, *bufB;
-    CHK(hipMalloc(&bufA, user * 3));
-    CHK(hipMalloc(&bufB, user * 3));
-    fill(bufA, user * 3, 12345);
-
-    if (getenv("KB_STATIC")) {
-        constexpr int K = 4;
-        constexpr uint32_t MASK = 0x3C;
         const uint64_t nst = user / (K * ECD_CHUNK);
         proto::InPtrs ip;
         ecd_combine_desc_t d;
@@ -220,7 +208,7 @@ int main(int argc, char **argv)
         d.in_stride = ECD_CHUNK;
         d.out_stride = (uint64_t)K * ECD_CHUNK;
         constexpr proto::Mat M = proto::decode_matrix<K, MASK>();
-        printf("inv 0x3C:");
+        printf("inv 0x%X:", MASK);
         for (int r = 0; r < K; ++r)
             for (int p = 0; p < K; ++p)
                 printf(" %02x", M.m[r][p]);
@@ -243,10 +231,8 @@ int main(int argc, char **argv)
         const double bytes = 2.0 * nst * K * ECD_CHUNK;
         const size_t ob = (size_t)nst * K * ECD_CHUNK;
         std::vector<Variant> v;
-        v.push_back({"combine TS2 NW4 GLDS (shipped)", bytes, [=](hipStream_t st) {
-                         const size_t lds = (size_t)K * 8 * 2 * ECD_CHUNK;
-                         hipLaunchKernelGGL((ec_combine<4, 2, 4, false, false>),
-                                            dim3((u32)((nst + 15) / 16)), dim3(256), lds, st, a);
+        v.push_back({"combine (shipped launcher)", bytes, [=](hipStream_t st) {
+                         ecdk_combine(st, &d);
                      }, bufB, ob});
         auto addst = [&](const char *nm, auto kern, int W) {
             const uint64_t g = (nst * (16 / W) + kBlock - 1) / kBlock;
@@ -255,10 +241,35 @@ int main(int argc, char **argv)
                                                 nst);
                          }, bufB, ob});
         };
-        addst("static W1", proto::ec_decode_static<K, MASK, 1>, 1);
-        addst("static W2", proto::ec_decode_static<K, MASK, 2>, 2);
-        addst("static W4", proto::ec_decode_static<K, MASK, 4>, 4);
-        run_group("decode 4+2 mask 0x3C", v, rounds, iters, s);
+        addst("static W1", proto::ec_decode_static<K, MASK, 1, false>, 1);
+        addst("static W1 NTS", proto::ec_decode_static<K, MASK, 1, true>, 1);
+        if constexpr (K <= 8) {
+            addst("static W2", proto::ec_decode_static<K, MASK, 2, false>, 2);
+            addst("static W2 NTS", proto::ec_decode_static<K, MASK, 2, true>, 2);
+        }
+        char title[64];
+        snprintf(title, sizeof(title), "decode %d+x mask 0x%X", K, MASK);
+        run_group(title, v, rounds, iters, s);
+    }
+
+int main(int argc, char **argv)
+{
+    const double gib = argc > 1 ? atof(argv[1]) : 1.0;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 7;
+    const int iters = 10;
+    hipStream_t s;
+    CHK(hipStreamCreate(&s));
+    const uint64_t user = (uint64_t)(gib * (1ull << 30));
+    uint8_t *bufA, *bufB;
+    CHK(hipMalloc(&bufA, user * 3));
+    CHK(hipMalloc(&bufB, user * 3));
+    fill(bufA, user * 3, 12345);
+
+    if (getenv("KB_STATIC")) {
+        static_group<4, 0x3C>(bufA, bufB, user, rounds, iters, s);
+        static_group<8, 0xFF0>(bufA, bufB, user, rounds, iters, s);
+        static_group<8, 0xEB5>(bufA, bufB, user, rounds, iters, s);
+        static_group<16, 0xFFFF0>(bufA, bufB, user, rounds, iters, s);
     }
     if (getenv("KB_NTS")) {
     /* B) non-temporal stores vs default, at 1 GiB and at 64K-stripe batches */
