@@ -298,11 +298,13 @@ __device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
  * one lane address serves all 8 planes of an input (ds_read2st64_b64 with
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
-template <int K, int TS, int NW, bool MIXED, bool NTS>
+template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
-    constexpr int CW = 2;                /* dwords per plane per lane (compute) */
+    /* CW: dwords per plane per lane in the compute phase; a wave item covers
+     * SPI = 4*CW stripes of one output row */
+    constexpr u32 LPS = 16 / CW, SPI = 64 / LPS, IPT = T / SPI;
     constexpr u32 NI = K * T * 32 / 64;  /* LDS-DMA wave instructions per tile */
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
@@ -342,11 +344,11 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     __syncthreads();
 
     /* compute: (row, 8-stripe subtile) items spread over the NW waves */
-    const u32 cs = lane >> 3, cc = lane & 7u;
-    const u32 items = a.rows * TS;
+    const u32 cs = lane / LPS, cc = lane % LPS;
+    const u32 items = a.rows * IPT;
     for (u32 it = wave; it < items; it += NW) {
-        const u32 r = it / TS, s = (it % TS) * 8u + cs;
-        const uint8_t *col = lds + s * 64u + cc * 8u;
+        const u32 r = it / IPT, s = (it % IPT) * SPI + cs;
+        const uint8_t *col = lds + s * 64u + cc * (4u * CW);
         /* the row's coefficients: up to 4 words, loaded once into SGPRs */
         const u32 rw = pb + a.kw * (1 + r);
         const u32 w0 = a.pat[rw];
@@ -356,7 +358,9 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         u32 acc[8][CW], y[8][CW];
 #pragma unroll
         for (int b = 0; b < 8; ++b)
-            acc[b][0] = acc[b][1] = 0;
+#pragma unroll
+            for (int w = 0; w < CW; ++w)
+                acc[b][w] = 0;
         for (u32 p = 0; p < k; ++p) {
             const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
             const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
@@ -364,16 +368,13 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                 continue;
             const uint8_t *src = col + p * (T * ECD_CHUNK);
 #pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const uint2 t = *reinterpret_cast<const uint2 *>(src + (u32)b * (T * 64u));
-                y[b][0] = t.x;
-                y[b][1] = t.y;
-            }
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
             ecgf::mul_xor_rt<CW>(c, acc, y);
         }
         const uint64_t ost = t0 + s;
         if (ost < a.nstripes)
-            store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+            store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
     }
 }
 

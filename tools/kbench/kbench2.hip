@@ -397,10 +397,15 @@ int main(int argc, char **argv)
             addd("NW8", ec_combine<8, 1, 8, false, false>, 1, 8);
             addd("NW4 NTS", ec_combine<8, 1, 4, false, true>, 1, 4);
             addd("NW16 NTS", ec_combine<8, 1, 16, false, true>, 1, 16);
+            addd("NW4 NTS CW1", ec_combine<8, 1, 4, false, true, 1>, 1, 4);
+            addd("NW8 NTS CW1", ec_combine<8, 1, 8, false, true, 1>, 1, 8);
         } else {
             addd("NW8 NTS (shipped)", ec_combine<16, 1, 8, false, true>, 1, 8);
             addd("NW16 NTS", ec_combine<16, 1, 16, false, true>, 1, 16);
             addd("NW16", ec_combine<16, 1, 16, false, false>, 1, 16);
+            addd("NW16 NTS CW1", ec_combine<16, 1, 16, false, true, 1>, 1, 16);
+            addd("NW8 NTS CW1", ec_combine<16, 1, 8, false, true, 1>, 1, 8);
+            addd("TS2 NW16 NTS CW1", ec_combine<16, 2, 16, false, true, 1>, 2, 16);
         }
         char title[96];
         snprintf(title, sizeof title, "decode %d+%d real inverse, %lu stripes", K,
