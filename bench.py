@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--extra", dest="extra", action="store_true", default=None)
     ap.add_argument("--no-extra", dest="extra", action="store_false")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-dist-extra", action="store_true",
+                    help="N > 1: skip the per-N 16+4 encode / self-heal / PCIe lines")
     ap.add_argument("--only", default=None,
                     help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R | heal:K+R | "
                          "rmw:K+R")
@@ -112,20 +114,21 @@ def run_decode(c, k, n, nbytes, mask, steps, warmup, seed, group=None):
                 rows=rows)
 
 
-def run_encode(c, k, n, nbytes, steps, warmup, seed):
+def run_encode(c, k, n, nbytes, steps, warmup, seed, group=None):
     torch = c.torch
     L, data, frags, nst = c.encoded(k, n, nbytes, seed)
     wall, kt = timed(torch, lambda: L.encode_device(c.dev.index, c.sp, nst, data, frags),
-                     steps, warmup)
+                     steps, warmup, group)
     rows = list(range(n - k + 1, n + 1))
     out = torch.empty_like(data)
     L.decode_device(c.dev.index, c.sp, nst, sum(1 << (r - 1) for r in rows),
                     [frags[r - 1] for r in rows], out)
     torch.cuda.synchronize()
-    return dict(kernel_s=kt, ok=bool(torch.equal(out, data)), user=nst * CHUNK * k)
+    return dict(wall=wall, kernel_s=kt, ok=bool(torch.equal(out, data)), user=nst * CHUNK * k)
 
 
-def run_mixed(c, k, n, nbytes, steps, warmup, seed, group_stripes=1024, nmasks=16):
+def run_mixed(c, k, n, nbytes, steps, warmup, seed, group_stripes=1024, nmasks=16,
+              group=None):
     """Self-heal reconstruct (configs[4]): every 1024-stripe group is decoded
     from its own k-of-n brick set, drawn (seeded) from `nmasks` masks."""
     import random
@@ -142,8 +145,9 @@ def run_mixed(c, k, n, nbytes, steps, warmup, seed, group_stripes=1024, nmasks=1
                       device=c.dev)
     out = torch.empty_like(data)
     wall, kt = timed(torch, lambda: L.decode_mixed_device(c.dev.index, c.sp, nst, group_stripes,
-                                                          gp, masks, frags, out), steps, warmup)
-    return dict(kernel_s=kt, ok=bool(torch.equal(out, data)), user=nst * CHUNK * k)
+                                                          gp, masks, frags, out), steps, warmup,
+                     group)
+    return dict(wall=wall, kernel_s=kt, ok=bool(torch.equal(out, data)), user=nst * CHUNK * k)
 
 
 def run_heal(c, k, n, nbytes, steps, warmup, seed):
@@ -190,9 +194,12 @@ def run_writev(c, k, n, nbytes, steps, warmup, seed):
     return dict(kernel_s=kt, ok=ok, user=nbytes, alg=nbytes + n * nst * CHUNK)
 
 
-def run_e2e(c, k, n, nbytes, steps):
+def run_e2e(c, k, n, nbytes, steps, group=None):
     """PCIe-inclusive: pinned host buffers in, pinned host buffers out, the
-    library's pipelined H2D / kernel / D2H path (all visible GPUs)."""
+    library's pipelined H2D / kernel / D2H path on the devices named by
+    EC_MI355X_HOST_DEVICES (main() sets it to this rank's GPU).  With a
+    group, each timed loop is bracketed by barriers and the max wall over
+    ranks is kept."""
     import ctypes
     import numpy as np
     g = c.g
@@ -218,18 +225,22 @@ def run_e2e(c, k, n, nbytes, steps):
         bufs.append(dout_p)
         with g.ECMatrixList(k, n) as L:
             L.encode_batch(nst, din_p, [p for p, _ in fr])          # warm
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                L.encode_batch(nst, din_p, [p for p, _ in fr])
-            te = (time.perf_counter() - t0) / steps
+
+            def loop(fn):
+                if group:
+                    group.barrier()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    fn()
+                el = time.perf_counter() - t0
+                return (group.max(el) if group else el) / steps
+
+            te = loop(lambda: L.encode_batch(nst, din_p, [p for p, _ in fr]))
             rows = list(range(n - k + 1, n + 1))
             mask = sum(1 << (r - 1) for r in rows)
             ins = [fr[r - 1][0] for r in rows]
             L.decode_batch(nst, mask, rows, ins, dout_p)
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                L.decode_batch(nst, mask, rows, ins, dout_p)
-            td = (time.perf_counter() - t0) / steps
+            td = loop(lambda: L.decode_batch(nst, mask, rows, ins, dout_p))
             ok = bool(np.array_equal(dout, din))
         res = dict(enc_user_GBps=round(gbps(S, te), 2), dec_user_GBps=round(gbps(S, td), 2),
                    ok=ok, bytes=S, buffers="pinned host (ec_method_host_alloc)")
@@ -285,8 +296,51 @@ def extra_configs(c, steps, warmup):
     r = run_writev(c, 4, 6, (1 << 30) + 777, st, warmup, 19)
     put("writev_rmw_4+2_1GiB_unaligned", r, r["alg"])
     torch.cuda.empty_cache()
-    ex["e2e_pcie_4+2_512MiB"] = run_e2e(c, 4, 6, 512 << 20, 3)
-    ex["e2e_pcie_16+4_512MiB"] = run_e2e(c, 16, 20, 512 << 20, 3)
+    for name, k, n in (("e2e_pcie_4+2_512MiB", 4, 6), ("e2e_pcie_16+4_512MiB", 16, 20)):
+        try:
+            ex[name] = run_e2e(c, k, n, 512 << 20, 3)
+        except Exception as exc:                 # reported, never fatal to the bench line
+            ex[name] = dict(error=repr(exc)[:200])
+    return ex
+
+
+def dist_configs(c, grp, steps, warmup):
+    """N > 1: the BASELINE configs defined on 2/4/8 GPUs, one rank per GPU,
+    each rank owning the stripe range of its share of the job (weak scaling,
+    no data-path collective).  Aggregate user GB/s = all ranks' user bytes x
+    steps / max-over-ranks wall time between barriers."""
+    torch = c.torch
+    st = max(3, steps // 2)
+    W = grp.world
+    ex = {}
+
+    def put(name, r, alg_per_user):
+        wall = grp.max(r["wall"])
+        ok = grp.all_ok(r["ok"])
+        agg = gbps(r["user"] * W * st, wall)
+        ex[name] = dict(user_GBps=round(agg, 1), per_gpu_user_GBps=round(agg / W, 1),
+                        hbm_frac_per_gpu=round(agg / W * alg_per_user / HBM_PEAK_GBPS, 4),
+                        ok=ok)
+
+    # configs[3]: 16+4 encode, stripe-range partitioned (2 GiB per GPU)
+    r = run_encode(c, 16, 20, 2 << 30, st, warmup, 15 + 101 * grp.rank, grp)
+    put("dist_enc_16+4_2GiB_per_gpu", r, 2.25)
+    del r
+    # configs[4]: self-heal reconstruct, mixed patterns (1 GiB per GPU)
+    r = run_mixed(c, 8, 12, 1 << 30, st, warmup, 17 + 101 * grp.rank, group=grp)
+    put("dist_selfheal_mixed16_8+4_1GiB_per_gpu", r, 2.0)
+    del r
+    torch.cuda.empty_cache()
+    # configs[3], PCIe-inclusive: pinned host buffers, 512 MiB per GPU
+    try:
+        e = run_e2e(c, 16, 20, 512 << 20, 3, grp)
+        ok = grp.all_ok(e["ok"])
+        ex["dist_e2e_pcie_16+4_512MiB_per_gpu"] = dict(
+            enc_user_GBps=round(e["enc_user_GBps"] * W, 2),
+            dec_user_GBps=round(e["dec_user_GBps"] * W, 2), ok=ok,
+            buffers="pinned host, one GPU per rank (EC_MI355X_HOST_DEVICES)")
+    except Exception as exc:                     # reported, never fatal to the bench line
+        ex["dist_e2e_pcie_16+4_512MiB_per_gpu"] = dict(error=repr(exc)[:200])
     return ex
 
 
@@ -311,7 +365,7 @@ def cpu_baseline(sample_frags, rows, k, n, budget_s=10.0):
             fn()
             passes += 1
             el = time.perf_counter() - t0
-            if el >= budget or passes >= 2000:
+            if el >= budget or passes >= 100000:
                 return passes, el
 
     out = np.empty(user, dtype=np.uint8)
@@ -350,6 +404,8 @@ def main():
     from glusterfs_amd.dist import Group, local_device_index
 
     dev_index = local_device_index()
+    # the host-buffer (PCIe) path of this rank uses its own GPU only
+    os.environ.setdefault("EC_MI355X_HOST_DEVICES", str(dev_index))
     torch.cuda.set_device(dev_index)          # before the process group (NCCL)
     grp = Group()
     dev = torch.device("cuda", dev_index)
@@ -418,6 +474,8 @@ def main():
     extra = args.extra if args.extra is not None else grp.world == 1
     if extra:
         out["extra"] = extra_configs(c, args.steps, args.warmup)
+    elif grp.world > 1 and not args.no_dist_extra:
+        out["extra"] = dist_configs(c, grp, args.steps, args.warmup)
     if frags_host is not None:
         out["cpu_baseline"] = cpu_baseline(frags_host, [3, 4, 5, 6], k, n)
     grp.barrier()

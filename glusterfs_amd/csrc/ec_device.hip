@@ -82,6 +82,31 @@ void set_err(const char *what, hipError_t e)
 std::once_flag g_dev_once;
 int g_ndev = 0;
 int g_dev_ids[kMaxDev];
+/* Devices the host-buffer entry points spread their stripes over (indices
+ * into g_dev_ids): all of them, or the comma list in EC_MI355X_HOST_DEVICES,
+ * e.g. to keep a client on its NUMA-local GPUs or one rank per GPU. */
+int g_nhost = 0;
+int g_host_devs[kMaxDev];
+
+void host_devices_from_env()
+{
+    const char *e = getenv("EC_MI355X_HOST_DEVICES");
+    bool seen[kMaxDev] = {};
+    while (e && *e) {
+        char *end = nullptr;
+        const long v = strtol(e, &end, 10);
+        if (end == e)
+            break;
+        if (v >= 0 && v < g_ndev && !seen[v]) {
+            seen[v] = true;
+            g_host_devs[g_nhost++] = (int)v;
+        }
+        e = *end == ',' ? end + 1 : end;
+    }
+    if (g_nhost == 0)
+        for (int i = 0; i < g_ndev; ++i)
+            g_host_devs[g_nhost++] = i;
+}
 
 void discover()
 {
@@ -96,6 +121,7 @@ void discover()
             continue; /* kernels are built for gfx950 only */
         g_dev_ids[g_ndev++] = i;
     }
+    host_devices_from_env();
     if (g_ndev == 0) {
         std::lock_guard<std::mutex> g(g_err_mu);
         g_err = "no gfx950 (MI355X) device visible";
@@ -612,10 +638,10 @@ int pick_device(uint64_t bytes)
 {
     static std::atomic<unsigned> rr{0};
     const unsigned start = rr.fetch_add(1);
-    int best = (int)(start % g_ndev);
+    int best = g_host_devs[start % g_nhost];
     uint64_t lo = g_inflight[best].load();
-    for (int i = 1; i < g_ndev; ++i) {
-        const int d = (int)((start + i) % g_ndev);
+    for (int i = 1; i < g_nhost; ++i) {
+        const int d = g_host_devs[(start + i) % g_nhost];
         const uint64_t v = g_inflight[d].load();
         if (v < lo) {
             lo = v;
@@ -633,8 +659,8 @@ int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
 {
     if (g_ndev == 0)
         return -ENODEV;
-    if (ndev <= 0 || ndev > g_ndev)
-        ndev = g_ndev;
+    if (ndev <= 0 || ndev > g_nhost)
+        ndev = g_nhost;
     if (ndev > 1 && bytes < split_min_bytes()) {
         const int d = pick_device(bytes);
         const int rc = fn(d, 0, nstripes);
@@ -649,10 +675,11 @@ int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
     for (int d = 0; d < ndev; ++d) {
         const uint64_t s0 = std::min(nstripes, units * d / ndev * align);
         const uint64_t s1 = std::min(nstripes, units * (d + 1) / ndev * align);
+        const int dev = g_host_devs[d];
         if (d == ndev - 1)
-            rcs[d] = fn(d, s0, s1);
+            rcs[d] = fn(dev, s0, s1);
         else
-            th.emplace_back([&, d, s0, s1] { rcs[d] = fn(d, s0, s1); });
+            th.emplace_back([&, d, dev, s0, s1] { rcs[d] = fn(dev, s0, s1); });
     }
     for (auto &t : th)
         t.join();

@@ -151,3 +151,32 @@ def test_register_errors(ec):
     assert lib.ec_method_host_unregister(ctypes.c_void_p(a.ctypes.data)) == -22
     with ec.host_registered(a):
         pass
+
+
+@pytest.mark.parametrize("spec", ["0", "0,0,7", "junk"])
+def test_host_devices_env(spec):
+    """EC_MI355X_HOST_DEVICES restricts the host-buffer path to a device
+    list (ec_device.hip host_devices_from_env); out-of-range or unparsable
+    entries are ignored and an empty set falls back to every device.  The
+    variable is read once per process, so each case runs in a child."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+import torch, glusterfs_amd as g, oracle as O
+k, n, nst = 4, 6, 4096
+data = O.fill_xorshift(512 * k * nst)
+frags = [np.empty(512 * nst, np.uint8) for _ in range(n)]
+with g.ECMatrixList(k, n) as L:
+    L.encode_batch(nst, data, frags)
+want = O.encode(k, n, data)
+assert all(np.array_equal(a, b) for a, b in zip(frags, want))
+print("ok")
+''' % (root, os.path.join(root, "oracle"))
+    env = dict(os.environ, EC_MI355X_HOST_DEVICES=spec, EC_SPLIT_MIN_MB="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
