@@ -461,7 +461,7 @@ int launch_encode(hipStream_t st, const EncodeJob &j, const uint8_t *din, uint8_
     d.npatterns = 1;
     d.pat_bytes = j.k + j.n * j.k;
     memcpy(d.pat, j.enc_pat, d.pat_bytes);
-    return ecdk_combine(st, &d);
+    return ecdk_combine_host(st, &d);
 }
 
 int run_encode_dev(int dev, const EncodeJob &j)
@@ -603,7 +603,7 @@ int run_decode_dev(int dev, const DecodeJob &j)
                 d->group_pattern = s->pin_grp[slot];
                 d->group_shift = j.group_shift;
             }
-            bt.launch = [d](hipStream_t st) { return ecdk_combine(st, d.get()); };
+            bt.launch = [d](hipStream_t st) { return ecdk_combine_host(st, d.get()); };
             return 0;
         });
     release(s);

@@ -12,6 +12,8 @@ int ecdk_has_vander(uint32_t k, uint32_t n);
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                        const void *in, void *const *out, bool zc = false);
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d);
+/* the same on pinned host memory (host-buffer path, zero-copy over PCIe) */
+int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d);
 /* Partial-stripe writes: materialise bytes [o0, o0+n) (n % 16 == 0) of the
  * virtual input {head[0:b1) | user[0:b2-b1) | tail[...]} into dst, and the
  * fused Vandermonde encode that reads interior stripes from user directly. */

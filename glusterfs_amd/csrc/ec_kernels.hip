@@ -194,3 +194,46 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
         return launch_combine<8, 1, 4, 8, true>(s, a);
     return launch_combine<16, 1, 16, 16, true>(s, a);
 }
+
+/* Host-buffer path: every buffer is pinned host memory read / written over
+ * PCIe (ec_device.hip run_pipeline), so the zero-copy combine with whole
+ * 1 KiB request runs; default (not non-temporal) stores there, which cost
+ * 12 % on the link (profiles/kbench_r01_zc.log). */
+int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
+{
+    CombineArgs a;
+    int rc = ecdk_pack_args(d, &a);
+    if (rc)
+        return rc;
+    if (d->k + d->rows > 16) {
+        if (d->k <= 4)
+            return launch_combine<4, 1, 8, 8, false>(s, a);
+        if (d->k <= 8)
+            return launch_combine<8, 1, 4, 8, false>(s, a);
+        return launch_combine<16, 1, 16, 16, false>(s, a);
+    }
+    const uint64_t g = (a.nstripes + 7) / 8;
+    if (g == 0)
+        return 0;
+    if (g > 0x7fffffffull)
+        return -EINVAL;
+    const size_t lds = (size_t)(d->k + d->rows) * 8 * ECD_CHUNK;
+    constexpr int NW = 8;
+    if (d->k <= 4) {
+        if (a.group_pattern)
+            hipLaunchKernelGGL((ec_combine_zc<4, NW, true>), dim3((u32)g), dim3(NW * 64), lds, s, a);
+        else
+            hipLaunchKernelGGL((ec_combine_zc<4, NW, false>), dim3((u32)g), dim3(NW * 64), lds, s, a);
+    } else if (d->k <= 8) {
+        if (a.group_pattern)
+            hipLaunchKernelGGL((ec_combine_zc<8, NW, true>), dim3((u32)g), dim3(NW * 64), lds, s, a);
+        else
+            hipLaunchKernelGGL((ec_combine_zc<8, NW, false>), dim3((u32)g), dim3(NW * 64), lds, s, a);
+    } else {
+        if (a.group_pattern)
+            hipLaunchKernelGGL((ec_combine_zc<16, NW, true>), dim3((u32)g), dim3(NW * 64), lds, s, a);
+        else
+            hipLaunchKernelGGL((ec_combine_zc<16, NW, false>), dim3((u32)g), dim3(NW * 64), lds, s, a);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

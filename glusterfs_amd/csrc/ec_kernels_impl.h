@@ -378,6 +378,105 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     }
 }
 
+/* Zero-copy variant for the host-buffer path, where every input and output
+ * lives in pinned host memory and the CUs read and write it over PCIe
+ * (ec_device.hip run_pipeline).  There the link, not HBM or the VALU, is the
+ * bound, and what matters is the request shape: ec_combine moves 64-byte
+ * plane segments (stripe-strided reads, 8-byte-per-lane stores), which cost
+ * ~25 % of the link against whole-line streams (tools/kbench/kbench2 KB_ZC,
+ * profiles/kbench_r01_zc.log).  Here both directions are contiguous runs:
+ *  - staging: piece e (16 B) of input p of the tile is byte (e % 32) * 16 of
+ *    stripe e / 32, so with in_stride = 512 (fragments) one wave instruction
+ *    reads 1 KiB of consecutive host memory; the LDS tile is chunk-major
+ *    (input p, stripe s at (p * 8 + s) * 512), which LDS-DMA writes linearly;
+ *  - compute as in ec_combine (8 stripes x 8 lanes x 2 dwords per plane);
+ *    bank conflicts of the chunk-major reads are hidden by the link;
+ *  - output: rows are assembled in a second LDS tile and written back with
+ *    16-byte lanes in the order of the destination (stripe-major data when
+ *    out_stride = rows * 512, otherwise row buffers), i.e. 1 KiB runs.
+ * LDS = (k + rows) * 4 KiB, so the launcher uses it for k + rows <= 16. */
+template <int K, int NW, bool MIXED>
+__global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
+{
+    constexpr u32 T = 8;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k, rows = a.rows;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    uint8_t *otile = lds + k * (T * ECD_CHUNK);
+
+    u32 pb = 0;
+    if constexpr (MIXED)
+        pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
+
+    /* stage: wave instruction ins = 1 KiB = stripes 2q, 2q+1 of input p */
+    const u32 ni = k * (T / 2);
+    for (u32 ins = wave; ins < ni; ins += NW) {
+        const u32 p = ins / (T / 2);
+        const u32 e = (ins % (T / 2)) * 64 + lane;   /* piece within input p */
+        const uint64_t st = t0 + e / 32;
+        if (st < a.nstripes) {
+            const u32 src = pat_byte(a, pb, p);
+            const uint8_t *g = a.in_base[src] + st * a.in_stride + (e % 32) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+        }
+    }
+    __syncthreads();
+
+    const u32 cs = lane >> 3, cc = lane & 7u;
+    for (u32 r = wave; r < rows; r += NW) {
+        const uint8_t *col = lds + cs * ECD_CHUNK + cc * 8u;
+        const u32 rw = pb + a.kw * (1 + r);
+        const u32 w0 = a.pat[rw];
+        const u32 w1 = K > 4 ? a.pat[rw + 1] : 0u;
+        const u32 w2 = K > 8 ? a.pat[rw + 2] : 0u;
+        const u32 w3 = K > 12 ? a.pat[rw + 3] : 0u;
+        u32 acc[8][2], y[8][2];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc[b][0] = acc[b][1] = 0;
+        for (u32 p = 0; p < k; ++p) {
+            const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
+            const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
+            if (c == 0)                  /* ec-code-c.c:11666-11676 */
+                continue;
+            const uint8_t *src = col + p * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<2>(src + (u32)b * 64u, y[b]);
+            ecgf::mul_xor_rt<2>(c, acc, y);
+        }
+        uint8_t *o = otile + (r * T + cs) * ECD_CHUNK + cc * 8u;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+    }
+    __syncthreads();
+
+    /* write back: 16-byte pieces in destination order */
+    const bool stripe_major = a.out_stride == (uint64_t)rows * ECD_CHUNK;
+    const u32 np = rows * T * 32;
+    for (u32 idx = tid; idx < np; idx += NW * 64) {
+        const u32 w = idx % 32;
+        u32 s, r;
+        if (stripe_major) {
+            s = idx / (rows * 32);
+            r = (idx / 32) % rows;
+        } else {
+            r = idx / (T * 32);
+            s = (idx / 32) % T;
+        }
+        const uint64_t ost = t0 + s;
+        if (ost < a.nstripes)
+            *reinterpret_cast<uint4 *>(a.out_base[r] + ost * a.out_stride + w * 16u) =
+                *reinterpret_cast<const uint4 *>(otile + (r * T + s) * ECD_CHUNK + w * 16u);
+    }
+}
+
 template <int TS>
 inline uint64_t combine_grid(uint64_t nstripes)
 {

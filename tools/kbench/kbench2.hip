@@ -271,6 +271,79 @@ int main(int argc, char **argv)
         static_group<8, 0xEB5>(bufA, bufB, user, rounds, iters, s);
         static_group<16, 0xFFFF0>(bufA, bufB, user, rounds, iters, s);
     }
+    if (getenv("KB_ZC")) {
+    /* Z) zero-copy decode: fragments and output in pinned host memory, read
+     * and written by the CUs over PCIe (the host-buffer path of
+     * ec_device.hip for pinned callers) -- combine variants */
+    for (const int K : {4, 8}) {
+        const uint64_t nst = (512ull << 20) / (K * ECD_CHUNK);
+        const proto::Mat M = K == 4 ? proto::decode_matrix<4, 0x3C>()
+                                    : proto::decode_matrix<8, 0xFF0>();
+        uint8_t *hin, *hout;
+        CHK(hipHostMalloc((void **)&hin, (size_t)nst * K * ECD_CHUNK, hipHostMallocDefault));
+        CHK(hipHostMalloc((void **)&hout, (size_t)nst * K * ECD_CHUNK, hipHostMallocDefault));
+        memset(hin, 0x5a, (size_t)nst * K * ECD_CHUNK);
+        ecd_combine_desc_t d;
+        memset(&d, 0, sizeof(d));
+        d.k = K;
+        d.rows = K;
+        d.nstripes = nst;
+        d.in_stride = ECD_CHUNK;
+        d.out_stride = (uint64_t)K * ECD_CHUNK;
+        for (int p = 0; p < K; ++p) {
+            d.in_base[p] = hin + (uint64_t)p * nst * ECD_CHUNK;
+            d.pat[p] = (uint8_t)p;
+        }
+        for (int r = 0; r < K; ++r) {
+            d.out_base[r] = hout + (uint64_t)r * ECD_CHUNK;
+            for (int p = 0; p < K; ++p)
+                d.pat[K + r * K + p] = (uint8_t)M.m[r][p];
+        }
+        d.npatterns = 1;
+        d.pat_bytes = K + K * K;
+        static CombineArgs a;
+        if (ecdk_pack_args(&d, &a))
+            exit(2);
+        const double ub = (double)nst * K * ECD_CHUNK; /* user bytes: GB/s = user rate */
+        std::vector<Variant> v;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        auto addz = [&](const char *nm, auto kern, int ts, int nw, int ldsmul = 1) {
+            v.push_back({nm, ub, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern, dim3((u32)(nst / (8 * ts))), dim3(64 * nw),
+                                                (size_t)K * 8 * ts * ECD_CHUNK * ldsmul, st, a);
+                         }, hout, ob});
+        };
+        v.push_back({"shipped device launcher", ub,
+                     [=](hipStream_t st) { ecdk_combine(st, &d); }, hout, ob});
+        v.push_back({"shipped host launcher", ub,
+                     [=](hipStream_t st) { ecdk_combine_host(st, &d); }, hout, ob});
+        if (K == 4) {
+            addz("TS1 NW8 NTS", ec_combine<4, 1, 8, false, true>, 1, 8);
+            addz("TS1 NW8", ec_combine<4, 1, 8, false, false>, 1, 8);
+            addz("TS1 NW4", ec_combine<4, 1, 4, false, false>, 1, 4);
+            addz("TS2 NW4", ec_combine<4, 2, 4, false, false>, 2, 4);
+            addz("TS2 NW8", ec_combine<4, 2, 8, false, false>, 2, 8);
+            addz("TS4 NW8", ec_combine<4, 4, 8, false, false>, 4, 8);
+            addz("TS4 NW16", ec_combine<4, 4, 16, false, false>, 4, 16);
+            addz("ZC NW4", ec_combine_zc<4, 4, false>, 1, 4, 2);
+            addz("ZC NW8", ec_combine_zc<4, 8, false>, 1, 8, 2);
+        } else {
+            addz("TS1 NW4 NTS", ec_combine<8, 1, 4, false, true>, 1, 4);
+            addz("TS1 NW4", ec_combine<8, 1, 4, false, false>, 1, 4);
+            addz("TS1 NW8", ec_combine<8, 1, 8, false, false>, 1, 8);
+            addz("TS2 NW8", ec_combine<8, 2, 8, false, false>, 2, 8);
+            addz("TS2 NW16", ec_combine<8, 2, 16, false, false>, 2, 16);
+            addz("ZC NW4", ec_combine_zc<8, 4, false>, 1, 4, 2);
+            addz("ZC NW8", ec_combine_zc<8, 8, false>, 1, 8, 2);
+        }
+        char title[96];
+        snprintf(title, sizeof title, "zero-copy decode %d+%d, 512 MiB pinned host (GB/s = user)",
+                 K, K / 2);
+        run_group(title, v, rounds, 3, s);
+        CHK(hipHostFree(hin));
+        CHK(hipHostFree(hout));
+    }
+    }
     if (getenv("KB_NTS")) {
     /* B) non-temporal stores vs default, at 1 GiB and at 64K-stripe batches */
     for (const double g : {gib, 0.0}) {
