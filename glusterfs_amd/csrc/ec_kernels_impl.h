@@ -134,11 +134,10 @@ struct FragPtrs {
 };
 
 /* Row I (evaluation point v = I + 1) of the reversed Vandermonde matrix. */
-template <int K, int W, int I, bool NTS>
-__device__ __forceinline__ void encode_row(const u32 (&x)[K][8][W], uint8_t *dst)
+template <int K, int W, int I>
+__device__ __forceinline__ void encode_row_acc(const u32 (&x)[K][8][W], u32 (&acc)[8][W])
 {
     constexpr u32 v = I + 1;
-    u32 acc[8][W];
     if constexpr (v == 1) {
         /* row 0 = XOR of all data chunks, as XOR3 chains */
 #pragma unroll
@@ -164,6 +163,13 @@ __device__ __forceinline__ void encode_row(const u32 (&x)[K][8][W], uint8_t *dst
         for (int j = 1; j < K; ++j)
             ecgf::horner<v, W>(acc, x[j]);
     }
+}
+
+template <int K, int W, int I, bool NTS>
+__device__ __forceinline__ void encode_row(const u32 (&x)[K][8][W], uint8_t *dst)
+{
+    u32 acc[8][W];
+    encode_row_acc<K, W, I>(x, acc);
     store_chunk<W, NTS>(dst, acc);
 }
 
@@ -211,38 +217,70 @@ inline uint64_t vander_grid(uint64_t nstripes)
  * Here a smaller grid strides over the stripes and each thread prefetches
  * its next stripe before it computes and stores the current one, so the
  * reads of one stripe overlap the writes of the previous one and the link
- * runs both directions at once (~45 GB/s each way, tools/kbench/zerocopy). */
+ * runs both directions at once (~45 GB/s each way, tools/kbench/zerocopy).
+ * The SW = 64/L consecutive stripes of a wave form one contiguous run of
+ * SW*512 bytes in every fragment; each output row is assembled in the
+ * wave's LDS slice and written back as 16-byte lanes, i.e. 1 KiB requests
+ * instead of 64-byte plane segments (the request shape is what the link
+ * charges for, see ec_combine_zc).  Loops and exits are wave-uniform so
+ * every lane of a run takes part in its write-back. */
 template <int K, int N, int W, int BS = kBlock>
 __global__ __launch_bounds__(BS) void ec_encode_vander_zc(const uint8_t *__restrict__ in,
                                                           const FragPtrs out, uint64_t nstripes)
 {
-    constexpr int L = 16 / W;
+    constexpr int L = 16 / W;             /* lanes per stripe        */
+    constexpr u32 SW = 64 / L;            /* stripes per wave        */
+    constexpr u32 RUN = SW * ECD_CHUNK;   /* bytes per fragment run  */
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BS / 64][RUN];
+    const u32 lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t gtid = (uint64_t)blockIdx.x * BS + threadIdx.x;
     const uint64_t step = (uint64_t)gridDim.x * (BS / L);
     const u32 colb = (u32)(gtid % L) * (4 * W);
+    const u32 sl = lane / L;
     uint64_t stripe = gtid / L;
-    if (stripe >= nstripes)
+    uint64_t wfirst = stripe - sl;        /* wave-uniform */
+    if (wfirst >= nstripes)
         return;
+    uint8_t *slice = lds[wv];
 
     u32 x[K][8][W];
-    const uint8_t *s = in + stripe * (uint64_t)(K * ECD_CHUNK) + colb;
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        load_chunk<W>(s + j * ECD_CHUNK, x[j]);
-    for (;;) {
-        const uint64_t nxt = stripe + step;
-        u32 y[K][8][W];
-        if (nxt < nstripes) {
-            const uint8_t *sn = in + nxt * (uint64_t)(K * ECD_CHUNK) + colb;
+    auto load = [&](uint64_t st, u32 (&d)[K][8][W]) {
+        if (st < nstripes) {
+            const uint8_t *sp = in + st * (uint64_t)(K * ECD_CHUNK) + colb;
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                load_chunk<W>(sn + j * ECD_CHUNK, y[j]);
+                load_chunk<W>(sp + j * ECD_CHUNK, d[j]);
         }
-        encode_rows<K, W, false>(std::make_integer_sequence<int, N>{}, x, out,
-                                 stripe * (uint64_t)ECD_CHUNK + colb);
-        if (nxt >= nstripes)
+    };
+    load(stripe, x);
+    for (;;) {
+        const uint64_t nxt = stripe + step, wnext = wfirst + step;
+        u32 y[K][8][W];
+        if (wnext < nstripes)
+            load(nxt, y);
+        static_for<0, N>([&](auto I) {
+            u32 acc[8][W];
+            encode_row_acc<K, W, decltype(I)::value>(x, acc);
+            store_chunk<W, false>(slice + sl * ECD_CHUNK + colb, acc);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint8_t *dst = out.p[decltype(I)::value] + wfirst * ECD_CHUNK;
+#pragma unroll
+            for (u32 j = 0; j < RUN / 1024; ++j) {
+                const u32 off = (j * 64 + lane) * 16;
+                if (wfirst + off / ECD_CHUNK < nstripes)
+                    *reinterpret_cast<uint4 *>(dst + off) =
+                        *reinterpret_cast<const uint4 *>(slice + off);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        });
+        if (wnext >= nstripes)
             break;
         stripe = nxt;
+        wfirst = wnext;
 #pragma unroll
         for (int j = 0; j < K; ++j)
 #pragma unroll
