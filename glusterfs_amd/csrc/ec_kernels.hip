@@ -31,6 +31,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "ec_kernels.h"
 #include "ec_kernels_impl.h"
 
@@ -205,7 +207,7 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
     int rc = ecdk_pack_args(d, &a);
     if (rc)
         return rc;
-    if (d->k + d->rows > 16) {
+    if (d->k + d->rows > 32) {
         if (d->k <= 4)
             return launch_combine<4, 1, 8, 8, false>(s, a);
         if (d->k <= 8)
@@ -230,6 +232,14 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
         else
             hipLaunchKernelGGL((ec_combine_zc<8, NW, false>), dim3((u32)g), dim3(NW * 64), lds, s, a);
     } else {
+        /* up to (16 + 16) * 4 KiB = 128 KiB of the CU's 160 KiB */
+        static std::once_flag once;
+        std::call_once(once, [] {
+            (void)hipFuncSetAttribute((const void *)ec_combine_zc<16, NW, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 128 << 10);
+            (void)hipFuncSetAttribute((const void *)ec_combine_zc<16, NW, false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 128 << 10);
+        });
         if (a.group_pattern)
             hipLaunchKernelGGL((ec_combine_zc<16, NW, true>), dim3((u32)g), dim3(NW * 64), lds, s, a);
         else

@@ -432,7 +432,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
  *  - output: rows are assembled in a second LDS tile and written back with
  *    16-byte lanes in the order of the destination (stripe-major data when
  *    out_stride = rows * 512, otherwise row buffers), i.e. 1 KiB runs.
- * LDS = (k + rows) * 4 KiB, so the launcher uses it for k + rows <= 16. */
+ * LDS = (k + rows) * 4 KiB, so the launcher uses it for k + rows <= 32. */
 template <int K, int NW, bool MIXED>
 __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
 {

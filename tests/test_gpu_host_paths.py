@@ -71,9 +71,11 @@ def _alloc(ec, kind, i):
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("k,n", [(4, 6), (8, 12), (5, 7)])
+@pytest.mark.parametrize("k,n", [(4, 6), (8, 12), (5, 7), (10, 13), (16, 20)])
 def test_encode_decode_host_kinds(ec, oracle, kind, k, n):
-    nst = 40000 if k <= 5 else 20000       # 2-3 staged batches, ragged tail
+    # 2-3 staged batches with a ragged tail; k + rows up to 32 exercises the
+    # 128 KiB-LDS zero-copy combine (10+3: generic encode, 16+4: decode)
+    nst = 40000 if k <= 5 else 20000 if k <= 8 else 9000
     data = rand_bytes(CHUNK * k * nst, seed=k * 7 + n)
     want = oracle.encode(k, n, data, nthreads=8)
     pools = {t: Bufs(ec, t) for t in ("pinned", "pageable", "misaligned", "registered")}
