@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--no-dist-extra", action="store_true",
                     help="N > 1: skip the per-N 16+4 encode / self-heal / PCIe lines")
     ap.add_argument("--only", default=None,
-                    help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R | heal:K+R | "
+                    help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R[:NMASKS] | heal:K+R | "
                          "rmw:K+R")
     return ap.parse_args()
 
@@ -291,6 +291,10 @@ def extra_configs(c, steps, warmup):
     put("dec_16+4_0xFFFF0_1GiB", r, 2 * r["user"])
     r = run_mixed(c, 8, 12, 1 << 30, st, warmup, 17)
     put("selfheal_mixed16_8+4_1GiB", r, 2 * r["user"])
+    # 64 masks of a 16+4 volume: past the kernel-argument space (7 matrices),
+    # the decode matrices come from the per-call device table
+    r = run_mixed(c, 16, 20, 1 << 30, st, warmup, 21, nmasks=64)
+    put("selfheal_mixed64_16+4_1GiB", r, 2 * r["user"])
     r = run_heal(c, 8, 12, 1 << 30, st, warmup, 18)
     put("heal_fused_8+4_regen4_1GiB", r, r["alg"])
     r = run_writev(c, 4, 6, (1 << 30) + 777, st, warmup, 19)
@@ -389,7 +393,8 @@ def only(c, spec, nbytes, steps, warmup):
     elif parts[0] == "dec":
         res = run_decode(c, k, n, nbytes, int(parts[2], 16), steps, warmup, 1)
     elif parts[0] == "mixed":
-        res = run_mixed(c, k, n, nbytes, steps, warmup, 1)
+        nm = int(parts[2]) if len(parts) > 2 else 16
+        res = run_mixed(c, k, n, nbytes, steps, warmup, 1, nmasks=nm)
     elif parts[0] == "rmw":
         res = run_writev(c, k, n, nbytes + 777, steps, warmup, 1)
     else:

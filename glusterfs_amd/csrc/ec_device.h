@@ -17,6 +17,7 @@ extern "C" {
 #define ECD_MAX_K 16u       /* EC_METHOD_MAX_FRAGMENTS (ec-method.h:23) */
 #define ECD_MAX_ROWS 32u    /* >= EC_MAX_NODES (31, ec.h:27-32) */
 #define ECD_MAX_PAT_BYTES 2048u
+#define ECD_MAX_PATTERNS 256u /* pattern ids are bytes */
 
 /* One launch of the generic GF(2^8) combination kernel:
  *   for every stripe t < nstripes and row r < rows:
@@ -24,7 +25,7 @@ extern "C" {
  * on 512-byte bit-sliced chunks.  A "pattern" is the packed byte string
  * {src[k], coef[rows][k]}; with group_pattern != NULL, stripe t uses pattern
  * group_pattern[t >> group_shift] (mixed per-stripe-range erasure patterns),
- * otherwise pattern 0. */
+ * otherwise pattern 0; ids >= npatterns are clamped to the last pattern. */
 typedef struct ecd_combine_desc {
     uint32_t k;             /* inputs per stripe (kernel template parameter) */
     uint32_t rows;          /* output rows per stripe                        */
@@ -38,6 +39,10 @@ typedef struct ecd_combine_desc {
     uint32_t npatterns;
     uint32_t pat_bytes;           /* bytes per packed pattern = k + rows*k   */
     uint32_t pad;
+    /* when non-NULL, the npatterns (<= ECD_MAX_PATTERNS) packed patterns are
+     * read from here instead of pat[] (host memory, read during the call);
+     * patterns beyond the kernel-argument space go to a device table */
+    const uint8_t *pat_ext;
     uint8_t pat[ECD_MAX_PAT_BYTES];
 } ecd_combine_desc_t;
 

@@ -592,7 +592,10 @@ int run_decode_dev(int dev, const DecodeJob &j)
             }
             d->npatterns = j.npatterns;
             d->pat_bytes = j.k + j.rows * j.k;
-            memcpy(d->pat, j.pats, (size_t)j.npatterns * d->pat_bytes);
+            if ((size_t)j.npatterns * d->pat_bytes <= ECD_MAX_PAT_BYTES)
+                memcpy(d->pat, j.pats, (size_t)j.npatterns * d->pat_bytes);
+            else
+                d->pat_ext = j.pats;   /* read at launch, inside this call */
             if (j.group_pattern) {
                 /* a is a multiple of the group size (B is, and s0 is aligned);
                  * the kernel reads the group-map slice from the slot's pinned
@@ -840,7 +843,7 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, uint
         return -ENODEV;
     if (nfrags == 0 || nfrags > ECD_MAX_ROWS || k == 0 || k > ECD_MAX_K || rows == 0 ||
         rows > ECD_MAX_ROWS || npatterns == 0 ||
-        (uint64_t)npatterns * (k + rows * k) > ECD_MAX_PAT_BYTES)
+        npatterns > ECD_MAX_PATTERNS)
         return -EINVAL;
     if (group_pattern && (group_shift < 3 || group_shift > 40))
         return -EINVAL;

@@ -31,7 +31,9 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "ec_kernels.h"
 #include "ec_kernels_impl.h"
@@ -71,7 +73,18 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
     if (g > 0x7fffffffull)
         return -EINVAL;
     const size_t lds = combine_lds<TS>(a.k);
-    if (a.group_pattern)
+    if (a.patg) {
+        /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
+        static std::once_flag once;
+        std::call_once(once, [] {
+            (void)hipFuncSetAttribute((const void *)ec_combine<K, TS, NWM, true, NTS, 2, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)(combine_lds<TS>(K) + kPatLdsBytes));
+        });
+        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, true>), dim3((u32)g),
+                           dim3(NWM * 64), lds + kPatLdsBytes, s, a);
+    }
+    else if (a.group_pattern)
         hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS>), dim3((u32)g), dim3(NWM * 64),
                            lds, s, a);
     else
@@ -148,14 +161,105 @@ int ecdk_encode_vander_rmw(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstri
     return -ENOTSUP;
 }
 
-/* Re-lay the packed byte patterns {src[k], coef[rows][k]} out in words. */
+namespace {
+
+const uint8_t *desc_pats(const ecd_combine_desc_t *d)
+{
+    return d->pat_ext ? d->pat_ext : d->pat;
+}
+
+/* Re-lay the packed byte patterns {src[k], coef[rows][k]} out in words:
+ * src[] then one word-aligned row per output, pwords words per pattern. */
+void pack_words(const ecd_combine_desc_t *d, u32 kw, u32 pwords, u32 *words)
+{
+    uint8_t *pb = reinterpret_cast<uint8_t *>(words);
+    const uint8_t *pats = desc_pats(d);
+    for (u32 q = 0; q < d->npatterns; ++q) {
+        const uint8_t *src = pats + (size_t)q * d->pat_bytes;
+        uint8_t *dst = pb + (size_t)q * pwords * 4;
+        memcpy(dst, src, d->k);
+        for (u32 r = 0; r < d->rows; ++r)
+            memcpy(dst + (size_t)(1 + r) * kw * 4, src + d->k + (size_t)r * d->k, d->k);
+    }
+}
+
+/* One upload of up to kPatWords pattern words into the device table, the
+ * words travelling in the kernel-argument segment (copied at launch, so the
+ * host buffer may go away; stream-ordered before the combine that reads it). */
+struct PatChunk {
+    u32 *dst;
+    u32 n;
+    u32 w[kPatWords];
+};
+
+__global__ __launch_bounds__(256) void ec_pat_upload(const PatChunk c)
+{
+    for (u32 i = threadIdx.x; i < c.n; i += 256u)
+        c.dst[i] = c.w[i];
+}
+
+/* Mixed calls whose patterns exceed the 2 KiB argument space: a per-call
+ * device table (stream-ordered allocation, freed after the combine). */
+int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32 **tab)
+{
+    const size_t nw = (size_t)a.pwords * a.npatterns;
+    std::vector<u32> w(nw, 0u);
+    pack_words(d, a.kw, a.pwords, w.data());
+    if (hipMallocAsync(reinterpret_cast<void **>(tab), nw * 4, s) != hipSuccess) {
+        *tab = nullptr;
+        (void)hipGetLastError();
+        return -ENOMEM;
+    }
+    PatChunk c;
+    for (size_t o = 0; o < nw; o += kPatWords) {
+        c.dst = *tab + o;
+        c.n = (u32)std::min<size_t>(kPatWords, nw - o);
+        memcpy(c.w, w.data() + o, (size_t)c.n * 4);
+        hipLaunchKernelGGL(ec_pat_upload, dim3(1), dim3(256), 0, s, c);
+    }
+    a.patg = *tab;
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+template <bool NTS>
+int launch_combine_k(hipStream_t s, const CombineArgs &a)
+{
+    /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
+    if (a.k <= 4)
+        return launch_combine<4, 1, 8, 8, NTS>(s, a);
+    if (a.k <= 8)
+        return launch_combine<8, 1, 4, 8, NTS>(s, a);
+    return launch_combine<16, 1, 16, 16, NTS>(s, a);
+}
+
+/* pack, then launch; -E2BIG from the packer means "use a device table" */
+template <bool NTS>
+int combine_any(hipStream_t s, const ecd_combine_desc_t *d)
+{
+    CombineArgs a;
+    int rc = ecdk_pack_args(d, &a);
+    u32 *tab = nullptr;
+    if (rc == -E2BIG && d->group_pattern)
+        rc = upload_table(s, d, a, &tab);
+    if (rc == 0)
+        rc = launch_combine_k<NTS>(s, a);
+    if (tab)
+        (void)hipFreeAsync(tab, s);
+    return rc;
+}
+
+} // namespace
+
+/* Validate and fill the kernel arguments.  Returns -E2BIG (header filled,
+ * patterns not packed) when the patterns exceed the argument space. */
 int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
 {
     if (d->k == 0 || d->k > ECD_MAX_K || d->rows == 0 || d->rows > ECD_MAX_ROWS)
         return -EINVAL;
     if (d->group_pattern && d->group_shift < 3)
         return -EINVAL; /* every tile of 8 stripes must sit in one group */
-    if (d->npatterns == 0 || (uint64_t)d->npatterns * d->pat_bytes > ECD_MAX_PAT_BYTES ||
+    if (d->npatterns == 0 || d->npatterns > ECD_MAX_PATTERNS ||
+        (!d->pat_ext && (uint64_t)d->npatterns * d->pat_bytes > ECD_MAX_PAT_BYTES) ||
         d->pat_bytes < d->k + d->rows * d->k)
         return -EINVAL;
     memcpy(a->in_base, d->in_base, sizeof(a->in_base));
@@ -164,37 +268,25 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
     a->out_stride = d->out_stride;
     a->nstripes = d->nstripes;
     a->group_pattern = d->group_pattern;
+    a->patg = nullptr;
     a->k = d->k;
     a->kw = (d->k + 3) / 4;
     a->rows = d->rows;
     a->group_shift = d->group_shift;
     a->pwords = a->kw * (1 + d->rows);
+    a->npatterns = d->npatterns;
+    if (a->pwords > kMaxPatWords)
+        return -EINVAL;
     if ((uint64_t)a->pwords * d->npatterns > kPatWords)
         return -E2BIG;
     memset(a->pat, 0, sizeof(a->pat));
-    uint8_t *pb = reinterpret_cast<uint8_t *>(a->pat);
-    for (u32 q = 0; q < d->npatterns; ++q) {
-        const uint8_t *src = d->pat + (size_t)q * d->pat_bytes;
-        uint8_t *dst = pb + (size_t)q * a->pwords * 4;
-        memcpy(dst, src, d->k);
-        for (u32 r = 0; r < d->rows; ++r)
-            memcpy(dst + (size_t)(1 + r) * a->kw * 4, src + d->k + (size_t)r * d->k, d->k);
-    }
+    pack_words(d, a->kw, a->pwords, a->pat);
     return 0;
 }
 
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
 {
-    CombineArgs a;
-    int rc = ecdk_pack_args(d, &a);
-    if (rc)
-        return rc;
-    /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
-    if (d->k <= 4)
-        return launch_combine<4, 1, 8, 8, true>(s, a);
-    if (d->k <= 8)
-        return launch_combine<8, 1, 4, 8, true>(s, a);
-    return launch_combine<16, 1, 16, 16, true>(s, a);
+    return combine_any<true>(s, d);
 }
 
 /* Host-buffer path: every buffer is pinned host memory read / written over
@@ -205,15 +297,10 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
 {
     CombineArgs a;
     int rc = ecdk_pack_args(d, &a);
+    if (rc == -E2BIG || (rc == 0 && d->k + d->rows > 32))
+        return combine_any<false>(s, d);   /* device pattern table / LDS limit */
     if (rc)
         return rc;
-    if (d->k + d->rows > 32) {
-        if (d->k <= 4)
-            return launch_combine<4, 1, 8, 8, false>(s, a);
-        if (d->k <= 8)
-            return launch_combine<8, 1, 4, 8, false>(s, a);
-        return launch_combine<16, 1, 16, 16, false>(s, a);
-    }
     const uint64_t g = (a.nstripes + 7) / 8;
     if (g == 0)
         return 0;

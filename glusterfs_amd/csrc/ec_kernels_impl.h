@@ -318,14 +318,84 @@ struct CombineArgs {
     uint8_t *out_base[ECD_MAX_ROWS];
     uint64_t in_stride, out_stride, nstripes;
     const uint8_t *group_pattern;
-    u32 k, kw, rows, group_shift, pwords;
+    const u32 *patg;        /* pattern table in device memory (PG kernels) */
+    u32 k, kw, rows, group_shift, pwords, npatterns;
     u32 pat[kPatWords];
 };
 
-__device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
+constexpr u32 kMaxPatWords = 128; /* one pattern: kw * (1 + rows) <= 4 * 32 */
+
+/* The words of the block's pattern (src[] then one row of coefficients per
+ * output).  PG = false: the kernel-argument segment, read by scalar loads.
+ * PG = true (mixed calls with more patterns than the 2 KiB argument space
+ * holds, e.g. > 7 erasure masks of a 16+4 volume): the pattern table in
+ * device memory -- the per-call cache of decode matrices.  Each block loads
+ * its pattern once (lane i: words i, i + 64) before any store is issued,
+ * keeps the src[] words in SGPRs for staging and parks the rest in LDS after
+ * the tile, where a coefficient word is one broadcast ds_read.  (A vector
+ * load per coefficient would need a vmcnt(0) wait that also drains the
+ * outstanding stores; keeping the words in VGPRs cost the k = 16 kernel its
+ * second block per CU: 68 VGPRs.) */
+template <bool PG>
+struct PatWords {
+    u32 pb;
+    u32 s0, s1, s2, s3;          /* PG: the src[] words */
+    const u32 *lp;               /* PG: the pattern in LDS */
+    __device__ __forceinline__ PatWords(const CombineArgs &a, u32 pat, u32 lane, uint8_t *lds_pat)
+    {
+        pb = pat * a.pwords;
+        if constexpr (PG) {
+            const u32 *t = a.patg + pb;
+            const u32 v0 = lane < a.pwords ? t[lane] : 0u;
+            const u32 v1 = lane + 64u < a.pwords ? t[lane + 64u] : 0u;
+            s0 = __builtin_amdgcn_readlane(v0, 0);
+            s1 = __builtin_amdgcn_readlane(v0, 1);
+            s2 = __builtin_amdgcn_readlane(v0, 2);
+            s3 = __builtin_amdgcn_readlane(v0, 3);
+            u32 *w = reinterpret_cast<u32 *>(lds_pat);
+            if (threadIdx.x < 64u) {   /* wave 0; visible after the staging barrier */
+                w[lane] = v0;
+                w[lane + 64u] = v1;
+            }
+            lp = w;
+        }
+    }
+    /* (the argument struct is passed in, not held: holding a reference to
+     * the kernel argument made the compiler copy all 2.6 KiB to scratch) */
+    __device__ __forceinline__ u32 word(const CombineArgs &a, u32 rel) const
+    {
+        if constexpr (PG)
+            return __builtin_amdgcn_readfirstlane(lp[rel]);
+        else
+            return a.pat[pb + rel];
+    }
+    __device__ __forceinline__ u32 byte(const CombineArgs &a, u32 idx) const
+    {
+        u32 w;
+        if constexpr (PG) {
+            /* branch-free pick (a select chain over the members became a
+             * load through a selected address, i.e. a scratch alloca) */
+            const u32 q = idx >> 2;
+            w = (s0 & (0u - (u32)(q == 0))) | (s1 & (0u - (u32)(q == 1))) |
+                (s2 & (0u - (u32)(q == 2))) | (s3 & (0u - (u32)(q == 3)));
+        } else {
+            w = a.pat[pb + (idx >> 2)];
+        }
+        return __builtin_amdgcn_readfirstlane((w >> ((idx & 3u) * 8u)) & 0xFFu);
+    }
+};
+
+constexpr size_t kPatLdsBytes = kMaxPatWords * 4; /* PG kernels: LDS after the tile */
+
+/* pattern id of the tile starting at stripe t0 (ids past the table clamp to
+ * the last pattern: a bad caller map must not fault the device) */
+template <bool MIXED>
+__device__ __forceinline__ u32 tile_pattern(const CombineArgs &a, uint64_t t0)
 {
-    const u32 w = a.pat[word + (idx >> 2)];
-    return __builtin_amdgcn_readfirstlane((w >> ((idx & 3u) * 8u)) & 0xFFu);
+    if constexpr (!MIXED)
+        return 0u;
+    const u32 id = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]);
+    return id < a.npatterns ? id : a.npatterns - 1u;
 }
 
 /* K: max inputs (k <= K); TS: tile = 8*TS stripes; NW: waves per block.
@@ -336,7 +406,7 @@ __device__ __forceinline__ u32 pat_byte(const CombineArgs &a, u32 word, u32 idx)
  * one lane address serves all 8 planes of an input (ds_read2st64_b64 with
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
-template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2>
+template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -351,9 +421,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
 
-    u32 pb = 0;
-    if constexpr (MIXED)
-        pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
+    const PatWords<PG> pw(a, tile_pattern<MIXED>(a, t0), lane, lds + k * (T * ECD_CHUNK));
 
     /* stage: every wave instruction (global_load_lds_dwordx4) fills 1 KiB of
      * LDS linearly = planes b, b+1 of input p for the tile's 8 stripes (T=8)
@@ -371,7 +439,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         const u32 s = (el >> 2) % T;
         const uint64_t st = t0 + s;
         if (st < a.nstripes) {
-            const u32 src = pat_byte(a, pb, p);
+            const u32 src = pw.byte(a, p);
             const uint8_t *g = a.in_base[src] + st * a.in_stride + ((el >> 2) / T) * 64u +
                                (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
@@ -388,11 +456,11 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         const u32 r = it / IPT, s = (it % IPT) * SPI + cs;
         const uint8_t *col = lds + s * 64u + cc * (4u * CW);
         /* the row's coefficients: up to 4 words, loaded once into SGPRs */
-        const u32 rw = pb + a.kw * (1 + r);
-        const u32 w0 = a.pat[rw];
-        const u32 w1 = K > 4 ? a.pat[rw + 1] : 0u;
-        const u32 w2 = K > 8 ? a.pat[rw + 2] : 0u;
-        const u32 w3 = K > 12 ? a.pat[rw + 3] : 0u;
+        const u32 rw = a.kw * (1 + r);
+        const u32 w0 = pw.word(a, rw);
+        const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+        const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
+        const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
         u32 acc[8][CW], y[8][CW];
 #pragma unroll
         for (int b = 0; b < 8; ++b)
@@ -445,9 +513,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
     const u32 lane = tid & 63u;
     uint8_t *otile = lds + k * (T * ECD_CHUNK);
 
-    u32 pb = 0;
-    if constexpr (MIXED)
-        pb = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]) * a.pwords;
+    const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
 
     /* stage: wave instruction ins = 1 KiB = stripes 2q, 2q+1 of input p */
     const u32 ni = k * (T / 2);
@@ -456,7 +522,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
         const u32 e = (ins % (T / 2)) * 64 + lane;   /* piece within input p */
         const uint64_t st = t0 + e / 32;
         if (st < a.nstripes) {
-            const u32 src = pat_byte(a, pb, p);
+            const u32 src = pw.byte(a, p);
             const uint8_t *g = a.in_base[src] + st * a.in_stride + (e % 32) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
@@ -468,11 +534,11 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
     const u32 cs = lane >> 3, cc = lane & 7u;
     for (u32 r = wave; r < rows; r += NW) {
         const uint8_t *col = lds + cs * ECD_CHUNK + cc * 8u;
-        const u32 rw = pb + a.kw * (1 + r);
-        const u32 w0 = a.pat[rw];
-        const u32 w1 = K > 4 ? a.pat[rw + 1] : 0u;
-        const u32 w2 = K > 8 ? a.pat[rw + 2] : 0u;
-        const u32 w3 = K > 12 ? a.pat[rw + 3] : 0u;
+        const u32 rw = a.kw * (1 + r);
+        const u32 w0 = pw.word(a, rw);
+        const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+        const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
+        const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
         u32 acc[8][2], y[8][2];
 #pragma unroll
         for (int b = 0; b < 8; ++b)

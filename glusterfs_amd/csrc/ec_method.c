@@ -730,8 +730,8 @@ int32_t
 ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_stripes,
                        const uintptr_t *group_masks, const void *const *frags, void *out)
 {
-    uint8_t pats[ECD_MAX_PAT_BYTES];
-    uintptr_t uniq[256];
+    uint8_t *pats;
+    uintptr_t uniq[ECD_MAX_PATTERNS];
     uint8_t *gp;
     uint64_t g, ngroups;
     uint32_t shift = 0, nu = 0, u, k, pb;
@@ -749,15 +749,19 @@ ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group
     pb = k + k * k;
     ngroups = (nstripes + group_stripes - 1) / group_stripes;
     gp = (uint8_t *)malloc(ngroups);
-    if (!gp)
+    pats = (uint8_t *)malloc((size_t)ECD_MAX_PATTERNS * pb);
+    if (!gp || !pats) {
+        free(gp);
+        free(pats);
         return -ENOMEM;
+    }
     rc = 0;
     for (g = 0; g < ngroups && rc == 0; g++) {
         for (u = 0; u < nu; u++)
             if (uniq[u] == group_masks[g])
                 break;
         if (u == nu) {
-            if ((nu + 1) * pb > ECD_MAX_PAT_BYTES || nu == 256) {
+            if (nu == ECD_MAX_PATTERNS) {
                 rc = -E2BIG;
                 break;
             }
@@ -769,6 +773,7 @@ ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group
     if (rc == 0)
         rc = ecd_decode_host(0, k, k, nstripes, list->rows, frags, out, NULL, nu, pats, gp,
                              shift);
+    free(pats);
     free(gp);
     return rc;
 }
@@ -988,6 +993,7 @@ ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
 {
     ecd_combine_desc_t d;
     uint32_t k, r, u, shift = 0;
+    uint8_t *ext;
     int rc;
 
     if (!list || !CTX(list) || !group_pattern || !masks || !frags || !out || nmasks == 0)
@@ -997,7 +1003,7 @@ ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
     while ((1ull << shift) < group_stripes)
         shift++;
     k = list->columns;
-    if ((uint64_t)nmasks * (k + k * k) > ECD_MAX_PAT_BYTES)
+    if (nmasks > ECD_MAX_PATTERNS)
         return -E2BIG;
     if (nstripes == 0)
         return 0;
@@ -1009,14 +1015,24 @@ ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
         d.in_base[u] = frags[u];
     for (r = 0; r < k; r++)
         d.out_base[r] = (uint8_t *)out + (uint64_t)r * EC_METHOD_CHUNK_SIZE;
-    for (u = 0; u < nmasks; u++) {
-        rc = mask_pattern(list, masks[u], d.pat + u * d.pat_bytes);
-        if (rc)
-            return rc;
+    /* more masks than the kernel-argument space holds: the launcher moves
+     * them to a device table (ec_kernels.hip upload_table) */
+    ext = NULL;
+    if ((uint64_t)nmasks * d.pat_bytes > ECD_MAX_PAT_BYTES) {
+        ext = (uint8_t *)malloc((size_t)nmasks * d.pat_bytes);
+        if (!ext)
+            return -ENOMEM;
+        d.pat_ext = ext;
     }
+    rc = 0;
+    for (u = 0; u < nmasks && rc == 0; u++)
+        rc = mask_pattern(list, masks[u], (ext ? ext : d.pat) + u * d.pat_bytes);
     d.group_pattern = group_pattern;
     d.group_shift = shift;
-    return ecd_combine(device, stream, &d);
+    if (rc == 0)
+        rc = ecd_combine(device, stream, &d);
+    free(ext);   /* packed into kernel arguments / uploaded during the call */
+    return rc;
 }
 
 int32_t

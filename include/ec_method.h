@@ -128,7 +128,8 @@ int32_t ec_method_decode_batch(ec_matrix_list_t *list, uint64_t nstripes,
  * are all n fragment buffers (nstripes*512 bytes each; entries of bricks no
  * group reads may be NULL), group g = stripes [g*group_stripes,
  * (g+1)*group_stripes) is decoded from the k bricks in group_masks[g].
- * group_stripes is a power of two >= 8.  out = nstripes*k*512 bytes. */
+ * group_stripes is a power of two >= 8.  out = nstripes*k*512 bytes.
+ * Up to 256 distinct masks per call (-E2BIG beyond). */
 int32_t ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes,
                                uint64_t group_stripes, const uintptr_t *group_masks,
                                const void *const *frags, void *out);
@@ -175,7 +176,9 @@ int32_t ec_method_decode_device(ec_matrix_list_t *list, int device, void *stream
                                 uint64_t nstripes, uintptr_t mask,
                                 const void *const *in, void *out);
 /* group_pattern: device array of nstripes/group_stripes bytes indexing
- * masks[0..nmasks) (nmasks is limited by the kernel-argument segment). */
+ * masks[0..nmasks), nmasks <= 256 (ids >= nmasks are clamped to the last
+ * mask).  Decode matrices that fit the 2 KiB kernel-argument segment travel
+ * there; more go to a per-call device table, asynchronously on `stream`. */
 int32_t ec_method_decode_mixed_device(ec_matrix_list_t *list, int device,
                                       void *stream, uint64_t nstripes,
                                       uint64_t group_stripes,

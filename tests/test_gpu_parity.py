@@ -242,3 +242,73 @@ def test_mixed_and_heal_device(ec, oracle, torch_cuda):
         ec.sync_device(0)
         for o, b in zip(outs, tgt):
             assert np.array_equal(o.cpu().numpy(), frags[b])
+
+
+def _distinct_masks(n, k, count, seed):
+    rng = np.random.default_rng(seed)
+    seen = []
+    while len(seen) < count:
+        m = sum(1 << int(b) for b in rng.choice(n, k, replace=False))
+        if m not in seen:
+            seen.append(m)
+    return seen
+
+
+@pytest.mark.parametrize("k,n,nmasks", [(16, 20, 40), (8, 12, 60), (16, 31, 50),
+                                        (4, 6, 15)])
+def test_decode_mixed_many_patterns_host(ec, oracle, k, n, nmasks):
+    """More erasure masks than the 2 KiB kernel-argument segment holds
+    (7 for 16+4, 28 for 8+4): the decode matrices go to a device table."""
+    group, ngroups = 8, 2 * nmasks + 3
+    nstripes = group * ngroups - 3
+    data = rand_bytes(CHUNK * k * nstripes, seed=k * 7 + nmasks)
+    frags = oracle.encode(k, n, data)
+    pool = _distinct_masks(n, k, nmasks, seed=nmasks)
+    masks = [pool[g % nmasks] for g in range(ngroups)]
+    out = np.zeros(CHUNK * k * nstripes, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed(nstripes, group, masks, frags, out)
+    assert np.array_equal(out, data)
+
+
+def test_decode_mixed_too_many_patterns(ec, oracle):
+    import errno
+    k, n = 3, 12                     # C(12, 3) = 220 < 256: accepted
+    pool = _distinct_masks(n, k, 220, seed=5)
+    nst = 8 * len(pool)
+    data = rand_bytes(CHUNK * k * nst, seed=6)
+    frags = oracle.encode(k, n, data)
+    out = np.zeros(CHUNK * k * nst, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed(nst, 8, pool, frags, out)
+        assert np.array_equal(out, data)
+    k, n = 4, 12                     # 257 distinct masks: -E2BIG
+    pool = _distinct_masks(n, k, 257, seed=7)
+    nst = 8 * len(pool)
+    data = rand_bytes(CHUNK * k * nst, seed=8)
+    frags = oracle.encode(k, n, data)
+    out = np.zeros(CHUNK * k * nst, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        with pytest.raises(OSError) as ei:
+            L.decode_mixed(nst, 8, pool, frags, out)
+        assert ei.value.errno == errno.E2BIG
+
+
+@pytest.mark.parametrize("k,n,nmasks", [(16, 20, 100), (8, 12, 30)])
+def test_decode_mixed_many_patterns_device(ec, oracle, torch_cuda, k, n, nmasks):
+    torch = torch_cuda
+    group = 16
+    ngroups = 3 * nmasks
+    nst = group * ngroups
+    data = rand_bytes(CHUNK * k * nst, seed=nmasks + 1)
+    frags = oracle.encode(k, n, data)
+    dfr = [torch.from_numpy(f).cuda() for f in frags]
+    masks = _distinct_masks(n, k, nmasks, seed=nmasks + 2)
+    ids = np.random.default_rng(3).integers(0, nmasks, ngroups).astype(np.uint8)
+    ids[-1] = 250                     # out of range: clamped to the last mask
+    gp = torch.from_numpy(ids).cuda()
+    out = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed_device(0, None, nst, group, gp, masks, dfr, out)
+        ec.sync_device(0)
+    assert np.array_equal(out.cpu().numpy(), data)
