@@ -615,28 +615,30 @@ __device__ __forceinline__ uint8_t rmw_byte(const RmwSrc &v, uint64_t o)
     return v.tail ? v.tail[o - v.b2] : 0;
 }
 
-/* W dwords of `p`, which may have any byte alignment: the aligned dwords
- * that cover [p, p + 4W) are loaded and funnel-shifted with v_alignbyte_b32.
- * Every loaded dword holds at least one byte of the range, so no load can
- * cross into a page the range does not touch. */
+/* W dwords of `p`, which may have any byte alignment.  ROCm runs gfx950 in
+ * unaligned access mode, so this is one global_load_dwordx{1,2,4} at the
+ * byte address (it touches exactly [p, p + 4W): no over-read into a page
+ * the range does not cover).  The earlier form -- W + 1 aligned dword loads
+ * funnel-shifted with v_alignbyte_b32 -- ran the 4+2 odd-address partial
+ * write at 0.51 of HBM peak (profiles/bench_r01_i.log). */
 template <int W>
 __device__ __forceinline__ void load_plane_unaligned(const uint8_t *p, u32 (&d)[W])
 {
-    const u32 mis = (u32)((uintptr_t)p & 3u);
-    const u32 *a = reinterpret_cast<const u32 *>((uintptr_t)p & ~(uintptr_t)3);
-    if (mis == 0) {
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-            d[w] = a[w];
-        return;
+    if constexpr (W == 1) {
+        __builtin_memcpy(&d[0], p, 4);
+    } else if constexpr (W == 2) {
+        uint2 v;
+        __builtin_memcpy(&v, p, 8);
+        d[0] = v.x;
+        d[1] = v.y;
+    } else {
+        uint4 v;
+        __builtin_memcpy(&v, p, 16);
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
     }
-    u32 t[W + 1];
-#pragma unroll
-    for (int w = 0; w <= W; ++w)
-        t[w] = a[w];
-#pragma unroll
-    for (int w = 0; w < W; ++w)
-        d[w] = __builtin_amdgcn_alignbyte(t[w + 1], t[w], mis);
 }
 
 /* Materialise bytes [o0, o0 + n) of the virtual input into dst (16 bytes
