@@ -56,6 +56,8 @@ def algorithmic(cfg, gib):
         return S, S * (k + k + r) // k
     if kind == "heal":
         return S, S + S * r // k
+    if kind == "rmw":                       # user bytes in + n fragments out
+        return S, S + S * (k + r) // k
     return S, 2 * S
 
 
