@@ -312,3 +312,26 @@ def test_decode_mixed_many_patterns_device(ec, oracle, torch_cuda, k, n, nmasks)
         L.decode_mixed_device(0, None, nst, group, gp, masks, dfr, out)
         ec.sync_device(0)
     assert np.array_equal(out.cpu().numpy(), data)
+
+
+@pytest.mark.parametrize("k,n", [(16, 20), (16, 18), (10, 13), (8, 12)])
+def test_decode_every_mask_random_fragments(ec, oracle, k, n):
+    """Exhaustive erasure coverage: every k-of-n brick set (4845 for 16+4)
+    decodes random (non-codeword) fragments exactly as the oracle's inverse,
+    i.e. the full linear map, 256 masks per mixed call (8-stripe groups)."""
+    group = 8
+    allm = [sum(1 << b for b in c) for c in itertools.combinations(range(n), k)]
+    with ec.ECMatrixList(k, n) as L:
+        for c0 in range(0, len(allm), 256):
+            masks = allm[c0:c0 + 256]
+            nst = group * len(masks)
+            frags = [rand_bytes(CHUNK * nst, seed=c0 * 31 + f) for f in range(n)]
+            out = np.zeros(CHUNK * k * nst, np.uint8)
+            L.decode_mixed(nst, group, masks, frags, out)
+            span = CHUNK * group
+            for g, m in enumerate(masks):
+                rows = oracle.mask_rows(m)
+                want = oracle.decode(k, rows, [frags[r - 1][g * span:(g + 1) * span]
+                                               for r in rows])
+                got = out[g * span * k:(g + 1) * span * k]
+                assert np.array_equal(got, want), "mask %#x" % m
