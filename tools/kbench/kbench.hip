@@ -203,6 +203,12 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     add("TS1 NW16 NTS", ec_combine<K, 1, 16, false, true>, 1, 16);
     if (K <= 4)
         add("TS2 NW4", ec_combine<K, 2, 4, false, false>, 2, 4);
+    if constexpr (K <= 8) {
+        add("TS2 NW8 NTS", ec_combine<K, 2, 8, false, true>, 2, 8);
+        add("TS2 NW16 NTS", ec_combine<K, 2, 16, false, true>, 2, 16);
+    }
+    if constexpr (K <= 4)
+        add("TS4 NW16 NTS", ec_combine<K, 4, 16, false, true>, 4, 16);
     add("TS1 NW4", ec_combine<K, 1, 4, false, false>, 1, 4);
     add("TS1 NW8", ec_combine<K, 1, 8, false, false>, 1, 8);
 }
