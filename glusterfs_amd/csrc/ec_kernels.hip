@@ -227,8 +227,17 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
     /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
     if (a.k <= 4)
         return launch_combine<4, 1, 8, 8, NTS>(s, a);
-    if (a.k <= 8)
+    if (a.k <= 8) {
+        /* Full decodes (rows > 4) of up to 128K stripes use 16-wave blocks:
+         * 64K-stripe batches (BASELINE configs[2]) 99.5 -> 91 us for 0xFF0,
+         * 108 -> 100 us for 0xEB5, same box, alternating libraries; at 1 GiB
+         * 4-wave blocks stay 2 % faster, at 128K stripes the two tie
+         * (profiles/kbench_r01_ts_*.log, ab_r01_nw16.log).  Heal-shaped
+         * calls (rows <= 4) keep 4 waves. */
+        if (a.rows > 4 && a.nstripes <= (1u << 17))
+            return launch_combine<8, 1, 16, 8, NTS>(s, a);
         return launch_combine<8, 1, 4, 8, NTS>(s, a);
+    }
     return launch_combine<16, 1, 16, 16, NTS>(s, a);
 }
 
