@@ -296,6 +296,43 @@ int main(int argc, char **argv)
         add_decode<8>(v, nst, fr, bufB, c);
         run_group("decode 8+4 dense", v, rounds, iters, s);
     }
+    {   /* 8+4 fused heal shape: k = 8 inputs, 4 output rows */
+        const int K = 8, RW = 4;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        ecd_combine_desc_t d;
+        memset(&d, 0, sizeof(d));
+        d.k = K;
+        d.rows = RW;
+        d.nstripes = nst;
+        d.in_stride = ECD_CHUNK;
+        d.out_stride = ECD_CHUNK;
+        for (int p = 0; p < K; ++p) {
+            d.in_base[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+            d.pat[p] = (uint8_t)p;
+        }
+        for (int r = 0; r < RW; ++r)
+            d.out_base[r] = bufB + (uint64_t)r * nst * ECD_CHUNK;
+        for (int i = 0; i < RW * K; ++i)
+            d.pat[K + i] = (uint8_t)(1 + (i * 97 + 31) % 255);
+        d.npatterns = 1;
+        d.pat_bytes = K + RW * K;
+        static CombineArgs a;
+        if (ecdk_pack_args(&d, &a))
+            exit(4);
+        const double bytes = (double)nst * (K + RW) * ECD_CHUNK;
+        const size_t lds = (size_t)K * 8 * ECD_CHUNK;
+        const uint64_t g = (nst + 7) / 8;
+        std::vector<Variant> v;
+        auto addh = [&](const char *nm, auto kern, int nw) {
+            v.push_back({nm, bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * nw), lds, st, a);
+                         }, bufB, (size_t)nst * RW * ECD_CHUNK});
+        };
+        addh("heal NW4 NTS", ec_combine<K, 1, 4, false, true>, 4);
+        addh("heal NW8 NTS", ec_combine<K, 1, 8, false, true>, 8);
+        addh("heal NW16 NTS", ec_combine<K, 1, 16, false, true>, 16);
+        run_group("heal 8+4 (regenerate 4 rows)", v, rounds, iters, s);
+    }
     {   /* 16+4 decode, dense */
         const uint64_t nst = user / (16 * ECD_CHUNK);
         uint8_t *fr[16];
