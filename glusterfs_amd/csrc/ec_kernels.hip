@@ -14,7 +14,8 @@
  *   combine  one tile per block, staged by LDS-DMA (global_load_lds_dwordx4)
  *            into a plane-major tile; outputs stored straight from registers.
  *            8-stripe tiles; 8 / 4 / 16 waves per block for k <= 4 / 8 / 16
- *            (8 waves for 8+4 mixed patterns).  At k = 16 two 16-wave
+ *            (8 waves for 8+4 mixed patterns, 16 for full 8+4 decodes of
+ *            up to 128K stripes).  At k = 16 two 16-wave
  *            blocks fill all 32 wave slots of a CU, which hides the
  *            compare-tree dispatch of the multiply.  Two back-to-back
  *            processes, 21 interleaved rounds (profiles/kbench_r01_nw*.log):
