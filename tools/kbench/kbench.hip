@@ -209,6 +209,8 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     }
     if constexpr (K <= 4)
         add("TS4 NW16 NTS", ec_combine<K, 4, 16, false, true>, 4, 16);
+    add("TS1 NW8 NTS CW1", ec_combine<K, 1, 8, false, true, 1>, 1, 8);
+    add("TS1 NW16 NTS CW1", ec_combine<K, 1, 16, false, true, 1>, 1, 16);
     add("TS1 NW4", ec_combine<K, 1, 4, false, false>, 1, 4);
     add("TS1 NW8", ec_combine<K, 1, 8, false, false>, 1, 8);
 }
