@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--no-dist-extra", action="store_true",
                     help="N > 1: skip the per-N 16+4 encode / self-heal / PCIe lines")
     ap.add_argument("--only", default=None,
-                    help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R[:NMASKS] | heal:K+R | "
+                    help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R[:NMASKS[:GROUP]] | heal:K+R | "
                          "rmw:K+R")
     return ap.parse_args()
 
@@ -394,7 +394,8 @@ def only(c, spec, nbytes, steps, warmup):
         res = run_decode(c, k, n, nbytes, int(parts[2], 16), steps, warmup, 1)
     elif parts[0] == "mixed":
         nm = int(parts[2]) if len(parts) > 2 else 16
-        res = run_mixed(c, k, n, nbytes, steps, warmup, 1, nmasks=nm)
+        gs = int(parts[3]) if len(parts) > 3 else 1024
+        res = run_mixed(c, k, n, nbytes, steps, warmup, 1, group_stripes=gs, nmasks=nm)
     elif parts[0] == "rmw":
         res = run_writev(c, k, n, nbytes + 777, steps, warmup, 1)
     else:

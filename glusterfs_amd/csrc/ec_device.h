@@ -35,7 +35,7 @@ typedef struct ecd_combine_desc {
     const void *in_base[ECD_MAX_ROWS];
     void *out_base[ECD_MAX_ROWS];
     const uint8_t *group_pattern; /* device array, or NULL                   */
-    uint32_t group_shift;         /* log2(stripes per pattern group), >= 3   */
+    uint32_t group_shift;         /* log2(stripes per pattern group)         */
     uint32_t npatterns;
     uint32_t pat_bytes;           /* bytes per packed pattern = k + rows*k   */
     uint32_t pad;

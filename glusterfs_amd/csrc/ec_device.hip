@@ -845,7 +845,7 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, uint
         rows > ECD_MAX_ROWS || npatterns == 0 ||
         npatterns > ECD_MAX_PATTERNS)
         return -EINVAL;
-    if (group_pattern && (group_shift < 3 || group_shift > 40))
+    if (group_pattern && group_shift > 40)
         return -EINVAL;
     DecodeJob base;
     base.k = k;

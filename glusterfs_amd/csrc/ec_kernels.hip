@@ -222,9 +222,26 @@ int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+/* pattern groups of 1, 2 or 4 stripes: the per-stripe waterfall kernel */
+int launch_combine_fine(hipStream_t s, const CombineArgs &a)
+{
+    const uint64_t g = (a.nstripes * 8 + 255) / 256;
+    if (g == 0)
+        return 0;
+    if (g > 0x7fffffffull)
+        return -EINVAL;
+    if (a.patg)
+        hipLaunchKernelGGL(ec_combine_fine<true>, dim3((u32)g), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(ec_combine_fine<false>, dim3((u32)g), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 template <bool NTS>
 int launch_combine_k(hipStream_t s, const CombineArgs &a)
 {
+    if (a.group_pattern && a.group_shift < 3)
+        return launch_combine_fine(s, a);
     /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
     if (a.k <= 4)
         return launch_combine<4, 1, 8, 8, NTS>(s, a);
@@ -266,8 +283,8 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
 {
     if (d->k == 0 || d->k > ECD_MAX_K || d->rows == 0 || d->rows > ECD_MAX_ROWS)
         return -EINVAL;
-    if (d->group_pattern && d->group_shift < 3)
-        return -EINVAL; /* every tile of 8 stripes must sit in one group */
+    if (d->group_pattern && d->group_shift > 40)
+        return -EINVAL; /* groups below 8 stripes run ec_combine_fine */
     if (d->npatterns == 0 || d->npatterns > ECD_MAX_PATTERNS ||
         (!d->pat_ext && (uint64_t)d->npatterns * d->pat_bytes > ECD_MAX_PAT_BYTES) ||
         d->pat_bytes < d->k + d->rows * d->k)
@@ -307,8 +324,8 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
 {
     CombineArgs a;
     int rc = ecdk_pack_args(d, &a);
-    if (rc == -E2BIG || (rc == 0 && d->k + d->rows > 32))
-        return combine_any<false>(s, d);   /* device pattern table / LDS limit */
+    if (rc == -E2BIG || (rc == 0 && (d->k + d->rows > 32 || (d->group_pattern && d->group_shift < 3))))
+        return combine_any<false>(s, d);   /* device pattern table / LDS limit / small groups */
     if (rc)
         return rc;
     const uint64_t g = (a.nstripes + 7) / 8;

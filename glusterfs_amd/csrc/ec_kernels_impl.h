@@ -581,6 +581,66 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
     }
 }
 
+/* Mixed-pattern combine for pattern groups smaller than a tile (1, 2 or 4
+ * stripes: a batch of small reads, each with its own set of live bricks).
+ * The 8 stripes of a wave may then need up to 8 different decode matrices,
+ * and the compare-tree multiply needs a wave-uniform coefficient.  So the
+ * wave runs a waterfall over its pattern ids: each pass takes the id of the
+ * first live lane, and the lanes holding that id decode their stripe with
+ * uniform coefficients while the others wait.  No LDS tile (its staging
+ * needs one src[] per tile): inputs are read straight from HBM, 8 lanes x
+ * 8 bytes per plane, and re-read per output row from L2.  Correctness path
+ * for a shape the tile kernels cannot take; groups of >= 8 stripes use
+ * ec_combine. */
+template <bool PG>
+__device__ __forceinline__ u32 fine_word(const CombineArgs &a, u32 i)
+{
+    if constexpr (PG)
+        return __builtin_amdgcn_readfirstlane(a.patg[i]);
+    else
+        return a.pat[i];
+}
+
+template <bool PG>
+__global__ __launch_bounds__(256) void ec_combine_fine(const CombineArgs a)
+{
+    const uint64_t gtid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t st = gtid >> 3;            /* 8 lanes per stripe */
+    const u32 cc = threadIdx.x & 7u;
+    if (st >= a.nstripes)
+        return;
+    u32 id = a.group_pattern[st >> a.group_shift];
+    if (id >= a.npatterns)                    /* clamp, as tile_pattern */
+        id = a.npatterns - 1u;
+    for (;;) {
+        const u32 cur = __builtin_amdgcn_readfirstlane(id);
+        if (id != cur)
+            continue;
+        const u32 pb = cur * a.pwords;
+        for (u32 r = 0; r < a.rows; ++r) {
+            u32 acc[8][2], y[8][2];
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                acc[b][0] = acc[b][1] = 0;
+            for (u32 p = 0; p < a.k; ++p) {
+                const u32 cw = fine_word<PG>(a, pb + a.kw * (1 + r) + (p >> 2));
+                const u32 c = __builtin_amdgcn_readfirstlane((cw >> ((p & 3u) * 8u)) & 0xFFu);
+                if (c == 0)                   /* ec-code-c.c:11666-11676 */
+                    continue;
+                const u32 sw = fine_word<PG>(a, pb + (p >> 2));
+                const u32 src = __builtin_amdgcn_readfirstlane((sw >> ((p & 3u) * 8u)) & 0xFFu);
+                const uint8_t *g = a.in_base[src] + st * a.in_stride + cc * 8u;
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    load_plane<2>(g + b * 64, y[b]);
+                ecgf::mul_xor_rt<2>(c, acc, y);
+            }
+            store_chunk<2, false>(a.out_base[r] + st * a.out_stride + cc * 8u, acc);
+        }
+        break;
+    }
+}
+
 template <int TS>
 inline uint64_t combine_grid(uint64_t nstripes)
 {

@@ -739,7 +739,7 @@ ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group
 
     if (!list || !CTX(list) || !group_masks || !frags || (!out && nstripes))
         return -EINVAL;
-    if (group_stripes < 8 || (group_stripes & (group_stripes - 1)))
+    if (group_stripes == 0 || (group_stripes & (group_stripes - 1)))
         return -EINVAL;
     while ((1ull << shift) < group_stripes)
         shift++;
@@ -998,7 +998,7 @@ ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
 
     if (!list || !CTX(list) || !group_pattern || !masks || !frags || !out || nmasks == 0)
         return -EINVAL;
-    if (group_stripes < 8 || (group_stripes & (group_stripes - 1)))
+    if (group_stripes == 0 || (group_stripes & (group_stripes - 1)))
         return -EINVAL;
     while ((1ull << shift) < group_stripes)
         shift++;

@@ -144,6 +144,29 @@ def test_decode_mixed_and_heal_host_kinds(ec, oracle, kind):
             p.close()
 
 
+@pytest.mark.parametrize("kind", ["pinned", "pageable"])
+def test_decode_mixed_small_groups_host_kinds(ec, oracle, kind):
+    """2-stripe pattern groups through the host-buffer pipeline (zero-copy
+    for pinned, staged for pageable), several batches."""
+    k, n, group = 4, 6, 2
+    nst = 40000 - 1
+    data = rand_bytes(CHUNK * k * nst, seed=19)
+    enc = oracle.encode(k, n, data, nthreads=8)
+    p = Bufs(ec, kind)
+    try:
+        frags = [p.new(CHUNK * nst, enc[i]) for i in range(n)]
+        out = p.new(data.size, 0)
+        ngroups = (nst + group - 1) // group
+        rng = np.random.default_rng(3)
+        pool_masks = [0x3C, 0x0F, 0x33, 0x2B, 0x1E]
+        masks = [pool_masks[i] for i in rng.integers(0, len(pool_masks), ngroups)]
+        with ec.ECMatrixList(k, n) as L:
+            L.decode_mixed(nst, group, masks, frags, out)
+        assert np.array_equal(out, data)
+    finally:
+        p.close()
+
+
 def test_register_errors(ec):
     import ctypes
     lib = ec.ec_method.lib

@@ -294,6 +294,54 @@ def test_decode_mixed_too_many_patterns(ec, oracle):
         assert ei.value.errno == errno.E2BIG
 
 
+def _check_groups(oracle, k, group, nst, masks, frags, out):
+    for g, m in enumerate(masks):
+        s0, s1 = g * group, min((g + 1) * group, nst)
+        rows = oracle.mask_rows(m)
+        want = oracle.decode(k, rows, [frags[r - 1][s0 * CHUNK:s1 * CHUNK] for r in rows])
+        assert np.array_equal(out[s0 * CHUNK * k:s1 * CHUNK * k], want), \
+            "group %d mask %#x" % (g, m)
+
+
+@pytest.mark.parametrize("k,n,group,nmasks", [(4, 6, 1, 5), (4, 6, 2, 15), (8, 12, 4, 9),
+                                              (16, 20, 1, 5), (16, 20, 2, 40), (3, 5, 4, 4),
+                                              (10, 13, 1, 12)])
+def test_decode_mixed_small_groups(ec, oracle, k, n, group, nmasks):
+    """Pattern groups below one 8-stripe tile (1, 2, 4 stripes: the per-stripe
+    waterfall kernel ec_combine_fine), incl. > 7 masks of 16+4 (device pattern
+    table) and a ragged last group.  Random fragments, so every group is
+    checked as the oracle's inverse applied to its bricks, not a round trip."""
+    ngroups = 61
+    nst = group * ngroups - (group - 1)
+    frags = [rand_bytes(CHUNK * nst, seed=group * 97 + f) for f in range(n)]
+    pool = _distinct_masks(n, k, nmasks, seed=group * 100 + k)
+    rng = np.random.default_rng(group + k)
+    masks = [pool[i] for i in rng.integers(0, nmasks, ngroups)]
+    out = np.zeros(CHUNK * k * nst, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed(nst, group, masks, frags, out)
+    _check_groups(oracle, k, group, nst, masks, frags, out)
+
+
+@pytest.mark.parametrize("k,n,group,nmasks", [(4, 6, 1, 15), (16, 20, 4, 30)])
+def test_decode_mixed_small_groups_device(ec, oracle, torch_cuda, k, n, group, nmasks):
+    torch = torch_cuda
+    ngroups = 301
+    nst = group * ngroups
+    frags = [rand_bytes(CHUNK * nst, seed=group * 13 + f) for f in range(n)]
+    dfr = [torch.from_numpy(f).cuda() for f in frags]
+    pool = _distinct_masks(n, k, nmasks, seed=nmasks + 9)
+    ids = np.random.default_rng(5).integers(0, nmasks, ngroups).astype(np.uint8)
+    ids[-1] = 251                     # out of range: clamped to the last mask
+    gp = torch.from_numpy(ids).cuda()
+    out = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed_device(0, None, nst, group, gp, pool, dfr, out)
+        ec.sync_device(0)
+    masks = [pool[min(int(i), nmasks - 1)] for i in ids]
+    _check_groups(oracle, k, group, nst, masks, frags, out.cpu().numpy())
+
+
 @pytest.mark.parametrize("k,n,nmasks", [(16, 20, 100), (8, 12, 30)])
 def test_decode_mixed_many_patterns_device(ec, oracle, torch_cuda, k, n, nmasks):
     torch = torch_cuda
