@@ -24,6 +24,7 @@ The JSON line also carries
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -135,6 +136,7 @@ def run_mixed(c, k, n, nbytes, steps, warmup, seed, group_stripes=1024, nmasks=1
     torch = c.torch
     L, data, frags, nst = c.encoded(k, n, nbytes, seed)
     rnd = random.Random(seed)
+    nmasks = min(nmasks, math.comb(n, k))
     masks = []
     while len(masks) < nmasks:
         m = sum(1 << b for b in rnd.sample(range(n), k))

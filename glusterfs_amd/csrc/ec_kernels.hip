@@ -225,7 +225,7 @@ int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32
 /* pattern groups of 1, 2 or 4 stripes: the per-stripe waterfall kernel */
 int launch_combine_fine(hipStream_t s, const CombineArgs &a)
 {
-    const uint64_t g = (a.nstripes * 8 + 255) / 256;
+    const uint64_t g = (a.nstripes * 16 + 255) / 256;
     if (g == 0)
         return 0;
     if (g > 0x7fffffffull)

@@ -587,9 +587,11 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
  * and the compare-tree multiply needs a wave-uniform coefficient.  So the
  * wave runs a waterfall over its pattern ids: each pass takes the id of the
  * first live lane, and the lanes holding that id decode their stripe with
- * uniform coefficients while the others wait.  No LDS tile (its staging
- * needs one src[] per tile): inputs are read straight from HBM, 8 lanes x
- * 8 bytes per plane, and re-read per output row from L2.  Correctness path
+ * uniform coefficients while the others wait.  One dword per plane per lane
+ * (16 lanes per stripe, 4 stripes per wave) bounds a wave at 4 passes: with
+ * 2 dwords (8 stripes per wave) 1-stripe groups took up to 8 passes of twice
+ * the code.  No LDS tile (its staging needs one src[] per tile): inputs are
+ * read straight from HBM and re-read per output row from L2.  Correctness path
  * for a shape the tile kernels cannot take; groups of >= 8 stripes use
  * ec_combine. */
 template <bool PG>
@@ -605,8 +607,8 @@ template <bool PG>
 __global__ __launch_bounds__(256) void ec_combine_fine(const CombineArgs a)
 {
     const uint64_t gtid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    const uint64_t st = gtid >> 3;            /* 8 lanes per stripe */
-    const u32 cc = threadIdx.x & 7u;
+    const uint64_t st = gtid >> 4;            /* 16 lanes per stripe, 1 dword per plane */
+    const u32 cc = threadIdx.x & 15u;
     if (st >= a.nstripes)
         return;
     u32 id = a.group_pattern[st >> a.group_shift];
@@ -618,10 +620,10 @@ __global__ __launch_bounds__(256) void ec_combine_fine(const CombineArgs a)
             continue;
         const u32 pb = cur * a.pwords;
         for (u32 r = 0; r < a.rows; ++r) {
-            u32 acc[8][2], y[8][2];
+            u32 acc[8][1], y[8][1];
 #pragma unroll
             for (int b = 0; b < 8; ++b)
-                acc[b][0] = acc[b][1] = 0;
+                acc[b][0] = 0;
             for (u32 p = 0; p < a.k; ++p) {
                 const u32 cw = fine_word<PG>(a, pb + a.kw * (1 + r) + (p >> 2));
                 const u32 c = __builtin_amdgcn_readfirstlane((cw >> ((p & 3u) * 8u)) & 0xFFu);
@@ -629,13 +631,13 @@ __global__ __launch_bounds__(256) void ec_combine_fine(const CombineArgs a)
                     continue;
                 const u32 sw = fine_word<PG>(a, pb + (p >> 2));
                 const u32 src = __builtin_amdgcn_readfirstlane((sw >> ((p & 3u) * 8u)) & 0xFFu);
-                const uint8_t *g = a.in_base[src] + st * a.in_stride + cc * 8u;
+                const uint8_t *g = a.in_base[src] + st * a.in_stride + cc * 4u;
 #pragma unroll
                 for (int b = 0; b < 8; ++b)
-                    load_plane<2>(g + b * 64, y[b]);
-                ecgf::mul_xor_rt<2>(c, acc, y);
+                    load_plane<1>(g + b * 64, y[b]);
+                ecgf::mul_xor_rt<1>(c, acc, y);
             }
-            store_chunk<2, false>(a.out_base[r] + st * a.out_stride + cc * 8u, acc);
+            store_chunk<1, false>(a.out_base[r] + st * a.out_stride + cc * 4u, acc);
         }
         break;
     }
