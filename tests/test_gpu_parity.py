@@ -323,6 +323,18 @@ def test_decode_mixed_small_groups(ec, oracle, k, n, group, nmasks):
     _check_groups(oracle, k, group, nst, masks, frags, out)
 
 
+@pytest.mark.parametrize("group", [0, 3, 12])
+def test_decode_mixed_bad_group_size(ec, oracle, group):
+    import errno
+    k, n, nst = 4, 6, 48
+    frags = [rand_bytes(CHUNK * nst, seed=f) for f in range(n)]
+    out = np.zeros(CHUNK * k * nst, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        with pytest.raises(OSError) as ei:
+            L.decode_mixed(nst, group, [0x3C] * nst, frags, out)
+        assert ei.value.errno == errno.EINVAL
+
+
 @pytest.mark.parametrize("k,n,group,nmasks", [(4, 6, 1, 15), (16, 20, 4, 30)])
 def test_decode_mixed_small_groups_device(ec, oracle, torch_cuda, k, n, group, nmasks):
     torch = torch_cuda
