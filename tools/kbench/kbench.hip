@@ -160,6 +160,117 @@ static void run_group(const char *title, std::vector<Variant> &vars, int rounds,
     fflush(stdout);
 }
 
+/* Candidate multiply without the 255-way compare tree:
+ * a wave takes R output rows at one dword per lane (16 lanes per stripe, 4
+ * stripes per item), forms the doublings F*2^i (i < 8) of each staged input
+ * once -- 3 XORs each in bit-sliced form (poly 0x11D), the rest renaming --
+ * and for every row adds the doublings its coefficient selects, two bits at
+ * a time: one XOR or XOR3 per plane per bit pair behind a uniform 4-way
+ * branch.  Staging is ec_combine's (plane-major LDS tile, 8 stripes). */
+__device__ __forceinline__ void kb_dbl(const u32 (&x)[8], u32 (&y)[8])
+{
+    y[0] = x[7];
+    y[1] = x[0];
+    y[2] = x[1] ^ x[7];
+    y[3] = x[2] ^ x[7];
+    y[4] = x[3] ^ x[7];
+    y[5] = x[4];
+    y[6] = x[5];
+    y[7] = x[6];
+}
+
+template <int K, int NW, int R, bool NTS>
+__global__ __launch_bounds__(NW * 64) void kb_combine_bp(const CombineArgs a)
+{
+    constexpr u32 T = 8;
+    constexpr u32 NI = K * T * 32 / 64;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+#pragma unroll
+    for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
+        const u32 ins = j * NW + wave;
+        if (ins >= NI)
+            break;
+        const u32 p = ins / (T / 2);
+        if (p >= k)
+            break;
+        const u32 el = (ins * 64 + lane) % (T * 32);
+        const u32 s = (el >> 2) % T;
+        const uint64_t st = t0 + s;
+        if (st < a.nstripes) {
+            const u32 src = __builtin_amdgcn_readfirstlane((a.pat[p >> 2] >> ((p & 3u) * 8u)) & 0xFFu);
+            const uint8_t *g = a.in_base[src] + st * a.in_stride + ((el >> 2) / T) * 64u +
+                               (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+        }
+    }
+    __syncthreads();
+
+    const u32 cs = lane >> 4, cc = lane & 15u;
+    const u32 items = ((a.rows + R - 1) / R) * 2;
+    for (u32 it = wave; it < items; it += NW) {
+        const u32 r0 = (it >> 1) * R, s = (it & 1u) * 4u + cs;
+        const uint8_t *col = lds + s * 64u + cc * 4u;
+        u32 acc[R][8];
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                acc[j][b] = 0;
+        for (u32 p = 0; p < k; ++p) {
+            u32 d[8][8];
+            const uint8_t *src = col + p * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                d[0][b] = *reinterpret_cast<const u32 *>(src + (u32)b * (T * 64u));
+#pragma unroll
+            for (int i = 1; i < 8; ++i)
+                kb_dbl(d[i - 1], d[i]);
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                if (r0 + j >= a.rows)
+                    break;
+                const u32 c = __builtin_amdgcn_readfirstlane(
+                    (a.pat[a.kw * (1 + r0 + j) + (p >> 2)] >> ((p & 3u) * 8u)) & 0xFFu);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const u32 sel = (c >> (2 * q)) & 3u;
+                    if (sel == 1) {
+#pragma unroll
+                        for (int b = 0; b < 8; ++b)
+                            acc[j][b] ^= d[2 * q][b];
+                    } else if (sel == 2) {
+#pragma unroll
+                        for (int b = 0; b < 8; ++b)
+                            acc[j][b] ^= d[2 * q + 1][b];
+                    } else if (sel == 3) {
+#pragma unroll
+                        for (int b = 0; b < 8; ++b)
+                            acc[j][b] = ecgf::xor3(acc[j][b], d[2 * q][b], d[2 * q + 1][b]);
+                    }
+                }
+            }
+        }
+        const uint64_t ost = t0 + s;
+        if (ost < a.nstripes) {
+#pragma unroll
+            for (int j = 0; j < R; ++j)
+                if (r0 + j < a.rows) {
+                    uint8_t *o = a.out_base[r0 + j] + ost * a.out_stride + cc * 4u;
+#pragma unroll
+                    for (int b = 0; b < 8; ++b)
+                        __builtin_nontemporal_store(acc[j][b], reinterpret_cast<u32 *>(o + b * 64));
+                }
+        }
+    }
+}
+
 /* decode k+r with the first r bricks missing, coefficients from the host
  * inverse (a dense k x k matrix is all we need for timing; correctness of
  * the math is covered by the parity tests -- here variants are compared
@@ -201,6 +312,10 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     add("TS1 NW4 NTS", ec_combine<K, 1, 4, false, true>, 1, 4);
     add("TS1 NW8 NTS", ec_combine<K, 1, 8, false, true>, 1, 8);
     add("TS1 NW16 NTS", ec_combine<K, 1, 16, false, true>, 1, 16);
+    add("BP R4 NW8 NTS", kb_combine_bp<K, 8, 4, true>, 1, 8);
+    add("BP R2 NW16 NTS", kb_combine_bp<K, 16, 2, true>, 1, 16);
+    add("BP R2 NW8 NTS", kb_combine_bp<K, 8, 2, true>, 1, 8);
+    add("BP R1 NW16 NTS", kb_combine_bp<K, 16, 1, true>, 1, 16);
     if (K <= 4)
         add("TS2 NW4", ec_combine<K, 2, 4, false, false>, 2, 4);
     if constexpr (K <= 8) {
