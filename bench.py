@@ -39,7 +39,9 @@ CHUNK = 512
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); without WORLD_SIZE in the environment and "
+                         "N > 1 the bench starts the N ranks itself (torch.distributed.run)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gib", type=float, default=1.0, help="user data per GPU per step")
@@ -405,8 +407,37 @@ def only(c, spec, nbytes, steps, warmup):
     print(json.dumps(dict(only=spec, kernel_ms=res["kernel_s"] * 1e3, ok=res["ok"])))
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` run without a launcher: start the N ranks as a
+    child torch.distributed.run (one process per GPU), before anything here
+    touches the GPU, and hand back its exit status (rank 0 prints the JSON
+    line to the shared stdout).  A child process, never exec: on this pool
+    replacing a process image is only safe before HIP initialises, and a
+    child keeps that true by construction."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus is not None and args.gpus > 1 and world_env is None:
+        sys.exit(launch_ranks(args.gpus))
+    if args.gpus is not None and int(world_env or 1) != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s: the ranks must match the GPUs"
+                 % (args.gpus, world_env))
     import torch
     import glusterfs_amd as g
     from glusterfs_amd.dist import Group, local_device_index

@@ -91,13 +91,17 @@ int g_host_devs[kMaxDev];
 void host_devices_from_env()
 {
     const char *e = getenv("EC_MI355X_HOST_DEVICES");
+    /* EC_MI355X_TEST_SPLIT=1 keeps repeated entries ("0,0"), so the
+     * in-library stripe split runs its multi-device code on one GPU (tests) */
+    const char *ts = getenv("EC_MI355X_TEST_SPLIT");
+    const bool dup = ts && *ts == '1';
     bool seen[kMaxDev] = {};
-    while (e && *e) {
+    while (e && *e && g_nhost < kMaxDev) {
         char *end = nullptr;
         const long v = strtol(e, &end, 10);
         if (end == e)
             break;
-        if (v >= 0 && v < g_ndev && !seen[v]) {
+        if (v >= 0 && v < g_ndev && (dup || !seen[v])) {
             seen[v] = true;
             g_host_devs[g_nhost++] = (int)v;
         }
@@ -132,6 +136,32 @@ hipStream_t pick_stream(void *stream)
 {
     return stream ? static_cast<hipStream_t>(stream) : hipStreamPerThread;
 }
+
+/* Every entry point that selects a device restores the calling thread's
+ * current device on return: the library shares the HIP runtime with its
+ * caller (torch, or a GlusterFS client that uses HIP itself), whose later
+ * allocations and launches must not move to another GPU. */
+class DeviceGuard {
+  public:
+    DeviceGuard()
+    {
+        if (hipGetDevice(&prev_) != hipSuccess) {
+            (void)hipGetLastError();
+            prev_ = -1;
+        }
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev_ >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev_)
+            (void)hipSetDevice(prev_);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+
+  private:
+    int prev_ = -1;
+};
 
 /* ------------------------------------------------- host-buffer pipeline */
 
@@ -217,6 +247,11 @@ class CopyPool {
         }
     }
 
+    /* A job stays at the front of the queue until all of its pieces are
+     * claimed, so every idle worker joins it (popping it on first sight
+     * left one helper per copy, whatever EC_COPY_THREADS said).  The owner
+     * erases it in run() once it is done; a worker that finds it fully
+     * claimed pops it. */
     void loop()
     {
         std::unique_lock<std::mutex> g(mu_);
@@ -225,12 +260,17 @@ class CopyPool {
             if (stop_)
                 return;
             Job *j = q_.front();
-            q_.pop_front(); /* claimed pieces are tracked by the job itself */
+            if (j->next.load() >= j->p->size()) {
+                q_.pop_front();
+                continue;
+            }
             ++j->active;
             g.unlock();
             work(*j);
             g.lock();
             --j->active;
+            if (!q_.empty() && q_.front() == j)
+                q_.pop_front();
             done_cv_.notify_all();
         }
     }
@@ -337,6 +377,7 @@ Stage *acquire(int dev)
     }
     Stage *s = new Stage;
     s->dev = dev;
+    DeviceGuard dg;
     bool ok = hipSetDevice(g_dev_ids[dev]) == hipSuccess &&
               hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess;
     for (int i = 0; ok && i < kSlots; ++i)
@@ -468,6 +509,7 @@ int run_encode_dev(int dev, const EncodeJob &j)
 {
     if (j.s1 <= j.s0)
         return 0;
+    DeviceGuard dg;
     HIPCHK(hipSetDevice(g_dev_ids[dev]));
     const uint64_t stripe_in = (uint64_t)j.k * ECD_CHUNK, cnt_all = j.s1 - j.s0;
     const bool in_direct =
@@ -478,8 +520,8 @@ int run_encode_dev(int dev, const EncodeJob &j)
         all_direct &= out_direct[i];
     }
     /* fully mapped jobs still run in batches so one launch stays short */
-    const uint64_t B = std::max<uint64_t>(
-        1, (all_direct ? 8 : 1) * pipe_batch_bytes() / stripe_in);
+    const uint64_t B = std::min<uint64_t>(
+        cnt_all, std::max<uint64_t>(1, (all_direct ? 8 : 1) * pipe_batch_bytes() / stripe_in));
     Stage *s = acquire(dev);
     if (!s)
         return -EIO;
@@ -527,6 +569,7 @@ int run_decode_dev(int dev, const DecodeJob &j)
 {
     if (j.s1 <= j.s0)
         return 0;
+    DeviceGuard dg;
     HIPCHK(hipSetDevice(g_dev_ids[dev]));
     const uint64_t out_stripe = (uint64_t)j.rows * ECD_CHUNK, cnt_all = j.s1 - j.s0;
     bool in_direct[ECD_MAX_ROWS] = {}, out_direct[ECD_MAX_ROWS] = {}, all_direct = true;
@@ -551,14 +594,17 @@ int run_decode_dev(int dev, const DecodeJob &j)
     const uint64_t grp = j.group_pattern ? (1ull << j.group_shift) : 1;
     if (j.group_pattern)
         B = std::max<uint64_t>(grp, B / grp * grp);
+    /* batches start at multiples of B (whole groups), but the staging slots
+     * never hold more than the data: Bs = stripes per slot */
+    const uint64_t Bs = std::min<uint64_t>(B, cnt_all);
     Stage *s = acquire(dev);
     if (!s)
         return -EIO;
-    int rc = grow(s->pin_in, s->cap_in, any_in_staged ? B * j.nfrags * ECD_CHUNK : 0);
+    int rc = grow(s->pin_in, s->cap_in, any_in_staged ? Bs * j.nfrags * ECD_CHUNK : 0);
     if (rc == 0)
-        rc = grow(s->pin_out, s->cap_out, all_direct ? 0 : B * out_stripe);
+        rc = grow(s->pin_out, s->cap_out, all_direct ? 0 : Bs * out_stripe);
     if (rc == 0)
-        rc = grow(s->pin_grp, s->cap_grp, j.group_pattern ? B / grp + 1 : 0);
+        rc = grow(s->pin_grp, s->cap_grp, j.group_pattern ? (Bs + grp - 1) / grp + 1 : 0);
     const uint64_t nb = (cnt_all + B - 1) / B;
     if (rc == 0)
         rc = run_pipeline(s, nb, [&](uint64_t b, int slot, Batch &bt) {
@@ -573,14 +619,14 @@ int run_decode_dev(int dev, const DecodeJob &j)
                 if (!j.frags[f])
                     continue;
                 bt.in.push_back({const_cast<uint8_t *>(j.frags[f]) + a * ECD_CHUNK,
-                                 cnt * ECD_CHUNK, !in_direct[f], (size_t)f * B * ECD_CHUNK});
+                                 cnt * ECD_CHUNK, !in_direct[f], (size_t)f * Bs * ECD_CHUNK});
                 d->in_base[f] = kaddr(s, slot, bt.in.back(), false);
             }
             if (j.outs) {
                 d->out_stride = ECD_CHUNK;
                 for (uint32_t r = 0; r < j.rows; ++r) {
                     bt.out.push_back({j.outs[r] + a * ECD_CHUNK, cnt * ECD_CHUNK,
-                                      !out_direct[r], (size_t)r * B * ECD_CHUNK});
+                                      !out_direct[r], (size_t)r * Bs * ECD_CHUNK});
                     d->out_base[r] = kaddr(s, slot, bt.out.back(), true);
                 }
             } else {
@@ -720,6 +766,7 @@ int ecd_encode_vander(int device, void *stream, uint32_t k, uint32_t n, uint64_t
 {
     if (ecd_device_count() <= device || device < 0)
         return -ENODEV;
+    DeviceGuard dg;
     HIPCHK(hipSetDevice(g_dev_ids[device]));
     return ecdk_encode_vander(pick_stream(stream), k, n, nstripes, in, out);
 }
@@ -728,6 +775,7 @@ int ecd_combine(int device, void *stream, const ecd_combine_desc_t *d)
 {
     if (ecd_device_count() <= device || device < 0)
         return -ENODEV;
+    DeviceGuard dg;
     HIPCHK(hipSetDevice(g_dev_ids[device]));
     return ecdk_combine(pick_stream(stream), d);
 }
@@ -736,6 +784,7 @@ int ecd_sync(int device, void *stream)
 {
     if (ecd_device_count() <= device || device < 0)
         return -ENODEV;
+    DeviceGuard dg;
     HIPCHK(hipSetDevice(g_dev_ids[device]));
     HIPCHK(hipStreamSynchronize(pick_stream(stream)));
     return 0;
@@ -804,6 +853,7 @@ int ecd_writev_encode_device(int device, void *stream, uint32_t k, uint32_t n, u
     } else if (ts) {
         ts += b2 - (nst - 1) * S; /* ec_merge_stripe_tail_locked, :1898-1908 */
     }
+    DeviceGuard dg;
     HIPCHK(hipSetDevice(g_dev_ids[device]));
     hipStream_t st = pick_stream(stream);
     const bool fused = ecdk_has_vander(k, n);

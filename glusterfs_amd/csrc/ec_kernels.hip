@@ -43,6 +43,27 @@ using namespace ecdev;
 
 namespace {
 
+/* hipFuncAttributeMaxDynamicSharedMemorySize is per device: set it once per
+ * (kernel, device), for the device current on the launching thread (a
+ * process-wide once-flag left every GPU but the first unconfigured). */
+int ensure_lds_limit(const void *kern, int bytes)
+{
+    static std::mutex mu;
+    static std::vector<std::pair<const void *, int>> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return -EIO;
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto &e : done)
+        if (e.first == kern && e.second == dev)
+            return 0;
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) !=
+        hipSuccess)
+        return -EIO;
+    done.emplace_back(kern, dev);
+    return 0;
+}
+
 template <int K, int N, int W, bool NTS = false>
 int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const *out, bool zc)
 {
@@ -76,12 +97,10 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
     const size_t lds = combine_lds<TS>(a.k);
     if (a.patg) {
         /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
-        static std::once_flag once;
-        std::call_once(once, [] {
-            (void)hipFuncSetAttribute((const void *)ec_combine<K, TS, NWM, true, NTS, 2, true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)(combine_lds<TS>(K) + kPatLdsBytes));
-        });
+        if (lds + kPatLdsBytes > (64u << 10) &&
+            ensure_lds_limit((const void *)ec_combine<K, TS, NWM, true, NTS, 2, true>,
+                             (int)(combine_lds<TS>(K) + kPatLdsBytes)) != 0)
+            return -EIO;
         hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, true>), dim3((u32)g),
                            dim3(NWM * 64), lds + kPatLdsBytes, s, a);
     }
@@ -347,13 +366,11 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
             hipLaunchKernelGGL((ec_combine_zc<8, NW, false>), dim3((u32)g), dim3(NW * 64), lds, s, a);
     } else {
         /* up to (16 + 16) * 4 KiB = 128 KiB of the CU's 160 KiB */
-        static std::once_flag once;
-        std::call_once(once, [] {
-            (void)hipFuncSetAttribute((const void *)ec_combine_zc<16, NW, true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 128 << 10);
-            (void)hipFuncSetAttribute((const void *)ec_combine_zc<16, NW, false>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 128 << 10);
-        });
+        if (lds > (64u << 10) &&
+            ensure_lds_limit(a.group_pattern ? (const void *)ec_combine_zc<16, NW, true>
+                                             : (const void *)ec_combine_zc<16, NW, false>,
+                             128 << 10) != 0)
+            return -EIO;
         if (a.group_pattern)
             hipLaunchKernelGGL((ec_combine_zc<16, NW, true>), dim3((u32)g), dim3(NW * 64), lds, s, a);
         else

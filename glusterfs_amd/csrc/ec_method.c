@@ -596,6 +596,31 @@ ec_method_update(xlator_t *xl, ec_matrix_list_t *list, const char *gen)
     return 0;
 }
 
+/* 1 when every non-NULL buffer of b[0..n) is on `dev` (-1: host memory).
+ * Host and device buffers cannot be mixed in one call: the kernels would
+ * read host addresses as device ones, the staging copies device addresses
+ * as host ones. */
+static int
+bufs_on(const void *const *b, uint32_t n, int dev)
+{
+    uint32_t i;
+
+    for (i = 0; i < n; i++)
+        if (b[i] && ecd_ptr_device(b[i]) != dev)
+            return 0;
+    return 1;
+}
+
+static uint32_t
+popcount_mask(uintptr_t m)
+{
+    uint32_t c = 0;
+
+    for (; m; m &= m - 1)
+        c++;
+    return c;
+}
+
 static int
 encode_any(ec_matrix_list_t *list, uint64_t nstripes, const void *in, void *const *out)
 {
@@ -726,6 +751,20 @@ mask_pattern(ec_matrix_list_t *list, uintptr_t mask, uint8_t *pat)
     return 0;
 }
 
+/* Every brick a mask reads must have a fragment buffer (frags[] may hold
+ * NULL for bricks no mask reads): a NULL here would be dereferenced by the
+ * kernel and fault the device instead of failing the call. */
+static int
+mask_frags_ok(const ec_matrix_list_t *list, uintptr_t mask, const void *const *frags)
+{
+    uint32_t b;
+
+    for (b = 0; b < list->rows; b++)
+        if (((mask >> b) & 1) && !frags[b])
+            return 0;
+    return 1;
+}
+
 int32_t
 ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_stripes,
                        const uintptr_t *group_masks, const void *const *frags, void *out)
@@ -763,6 +802,10 @@ ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group
         if (u == nu) {
             if (nu == ECD_MAX_PATTERNS) {
                 rc = -E2BIG;
+                break;
+            }
+            if (!mask_frags_ok(list, group_masks[g], frags)) {
+                rc = -EINVAL;
                 break;
             }
             rc = mask_pattern(list, group_masks[g], pats + nu * pb);
@@ -829,14 +872,19 @@ ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
         return -EINVAL;
     if (nstripes == 0)
         return 0;
+    if ((target_mask >> list->rows) != 0 || target_mask == 0)
+        return -EINVAL;
+    for (p = 0; p < list->columns; p++)
+        if (!in[p])
+            return -EINVAL;
     dev = ecd_ptr_device(in[0]);
+    if (!bufs_on(in, list->columns, dev) ||
+        !bufs_on((const void *const *)out, popcount_mask(target_mask), dev))
+        return -EINVAL;
     if (dev >= 0) {
         rc = ec_method_heal_device(list, dev, NULL, nstripes, mask, in, target_mask, out);
         return rc ? rc : ecd_sync(dev, NULL);
     }
-    for (p = 0; p < list->columns; p++)
-        if (ecd_ptr_device(in[p]) >= 0)
-            return -EINVAL;
     rc = heal_pattern(list, mask, rows, target_mask, pat, &nt);
     if (rc)
         return rc;
@@ -871,6 +919,17 @@ ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iove
     nst = (b2 + S - 1) / S;
     /* device buffers: the fused kernel (one contiguous user buffer) */
     dev = ecd_ptr_device(iov[0].iov_base);
+    {
+        const void *olds[2] = {old_head, old_tail};
+        for (c = 1; c < count; c++)
+            if (ecd_ptr_device(iov[c].iov_base) != dev)
+                return -EINVAL;
+        if (!bufs_on(olds, 2, dev) || !bufs_on((const void *const *)out, ctx->n, dev))
+            return -EINVAL;
+        for (i = 0; i < ctx->n; i++)
+            if (!out[i])
+                return -EINVAL;
+    }
     if (dev >= 0) {
         if (count != 1)
             return -EINVAL;
@@ -878,9 +937,6 @@ ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iove
                                            old_head, old_tail, out);
         return c ? c : ecd_sync(dev, NULL);
     }
-    for (i = 0; i < ctx->n; i++)
-        if (ecd_ptr_device(out[i]) >= 0)
-            return -EINVAL;
     if (nst == 1) { /* one stripe: its old content fills both ends */
         hs = hs ? hs : ts;
         ts = hs ? hs + b2 : NULL;
@@ -1026,7 +1082,9 @@ ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
     }
     rc = 0;
     for (u = 0; u < nmasks && rc == 0; u++)
-        rc = mask_pattern(list, masks[u], (ext ? ext : d.pat) + u * d.pat_bytes);
+        rc = mask_frags_ok(list, masks[u], frags)
+                 ? mask_pattern(list, masks[u], (ext ? ext : d.pat) + u * d.pat_bytes)
+                 : -EINVAL;
     d.group_pattern = group_pattern;
     d.group_shift = shift;
     if (rc == 0)

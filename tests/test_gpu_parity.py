@@ -395,3 +395,114 @@ def test_decode_every_mask_random_fragments(ec, oracle, k, n):
                                                for r in rows])
                 got = out[g * span * k:(g + 1) * span * k]
                 assert np.array_equal(got, want), "mask %#x" % m
+
+
+# --- device-resident kernels, exhaustively (the instantiations bench.py times) ---
+
+def _device_decode_masks(ec, oracle, torch, k, n, masks, nst, seed, nthreads=1):
+    """decode_batch on torch device buffers (ec_method_decode_device ->
+    ec_combine<K,TS,NW,false,NTS>) for every mask, on random fragments, each
+    output compared with the oracle's inverse applied to the same bricks."""
+    frags = [rand_bytes(CHUNK * nst, seed + i) for i in range(n)]
+    dfr = [torch.from_numpy(f).cuda() for f in frags]
+    out = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+    with ec.ECMatrixList(k, n) as L:
+        for m in masks:
+            rows = oracle.mask_rows(m)
+            out.fill_(0xA5)
+            L.decode_batch(nst, m, rows, [dfr[r - 1] for r in rows], out)
+            want = oracle.decode(k, rows, [frags[r - 1] for r in rows], nthreads=nthreads)
+            assert np.array_equal(out.cpu().numpy(), want), "mask %#x" % m
+
+
+@pytest.mark.parametrize("k,n,nst", [(4, 6, 77), (8, 12, 61), (2, 3, 40), (3, 5, 19)])
+def test_decode_device_every_mask(ec, oracle, torch_cuda, k, n, nst):
+    """All 15 masks of 4+2 and all 495 of 8+4 on the device-resident path."""
+    masks = [sum(1 << b for b in c) for c in itertools.combinations(range(n), k)]
+    _device_decode_masks(ec, oracle, torch_cuda, k, n, masks, nst, seed=k * 31 + n)
+
+
+def test_decode_device_sampled_masks_16p4(ec, oracle, torch_cuda):
+    """200 sampled masks of 16+4 on the device-resident path (k = 16 kernel)."""
+    k, n = 16, 20
+    allm = [sum(1 << b for b in c) for c in itertools.combinations(range(n), k)]
+    pick = np.random.default_rng(16).choice(len(allm), 200, replace=False)
+    _device_decode_masks(ec, oracle, torch_cuda, k, n, [allm[i] for i in pick], 45, seed=1604)
+
+
+@pytest.mark.parametrize("mask", [0xFF0, 0xAB5])
+def test_decode_device_8p4_large_batch(ec, oracle, torch_cuda, mask):
+    """More than 131,072 stripes of 8+4: the 4-wave-block instantiation the
+    launcher picks for large full decodes (ec_kernels.hip launch_combine_k)."""
+    _device_decode_masks(ec, oracle, torch_cuda, 8, 12, [mask], (1 << 17) + 77, seed=812,
+                         nthreads=8)
+
+
+def test_encode_device_large_batches(ec, oracle, torch_cuda):
+    """Device encode at sizes past one grid wave, every specialised geometry."""
+    torch = torch_cuda
+    for k, n, nst in ((4, 6, 300007), (8, 12, 70001), (16, 20, 20011)):
+        data = rand_bytes(CHUNK * k * nst, seed=nst)
+        want = oracle.encode(k, n, data, nthreads=8)
+        din = torch.from_numpy(data).cuda()
+        outs = [torch.empty(CHUNK * nst, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        with ec.ECMatrixList(k, n) as L:
+            L.encode_batch(nst, din, outs)
+        for i in range(n):
+            assert np.array_equal(outs[i].cpu().numpy(), want[i]), (k, n, i)
+
+
+# --- argument guards (ADVICE r01) --------------------------------------------
+
+def test_decode_mixed_null_fragment_rejected(ec, torch_cuda):
+    """A mask that reads a brick whose fragment is NULL fails with EINVAL on
+    the host and device paths instead of faulting the device."""
+    import errno
+    torch = torch_cuda
+    k, n, nst = 4, 6, 64
+    frags = [rand_bytes(CHUNK * nst, f) for f in range(n)]
+    frags[2] = None                                  # brick 2 absent
+    out = np.zeros(CHUNK * k * nst, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed(nst, 8, [0x3C] * 8, frags, out)          # 0x3C skips 0,1 only
+        with pytest.raises(OSError) as ei:
+            L.decode_mixed(nst, 8, [0x3C, 0x0F] * 4, frags, out)  # 0x0F reads brick 2
+        assert ei.value.errno == errno.EINVAL
+        dfr = [None if f is None else torch.from_numpy(f).cuda() for f in frags]
+        dout = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+        gp = torch.zeros(nst // 8, dtype=torch.uint8, device="cuda")
+        with pytest.raises(OSError) as ei:
+            L.decode_mixed_device(0, None, nst, 8, gp, [0x0F], dfr, dout)
+        assert ei.value.errno == errno.EINVAL
+
+
+def test_mixed_host_device_buffers_rejected(ec, torch_cuda):
+    import errno
+    torch = torch_cuda
+    k, n, nst = 4, 6, 16
+    with ec.ECMatrixList(k, n) as L:
+        din = [torch.zeros(CHUNK * nst, dtype=torch.uint8, device="cuda") for _ in range(k)]
+        hout = [np.zeros(CHUNK * nst, np.uint8) for _ in range(2)]
+        with pytest.raises(OSError) as ei:              # device in, host out
+            L.heal(nst, 0x3C, din, 0x03, hout)
+        assert ei.value.errno == errno.EINVAL
+        hin = [np.zeros(CHUNK * nst, np.uint8) for _ in range(k)]
+        hin[3] = din[3]
+        with pytest.raises(OSError) as ei:              # one device input among host ones
+            L.heal(nst, 0x3C, hin, 0x03, hout)
+        assert ei.value.errno == errno.EINVAL
+        user = torch.zeros(CHUNK * k * 3, dtype=torch.uint8, device="cuda")
+        with pytest.raises(OSError) as ei:              # device user data, host fragments
+            L.writev_encode(0, user, None, None, [np.zeros(CHUNK * 3, np.uint8)] * n)
+        assert ei.value.errno == errno.EINVAL
+
+
+def test_decode_mixed_group_larger_than_call(ec, oracle):
+    """group_stripes far above nstripes: one group, staging sized by the data."""
+    k, n, nst = 4, 6, 100
+    data = rand_bytes(CHUNK * k * nst, 12)
+    frags = oracle.encode(k, n, data)
+    out = np.zeros(CHUNK * k * nst, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed(nst, 1 << 20, [0xF0 >> 2], frags, out)
+    assert np.array_equal(out, data)
