@@ -430,7 +430,7 @@ def test_decode_device_sampled_masks_16p4(ec, oracle, torch_cuda):
     _device_decode_masks(ec, oracle, torch_cuda, k, n, [allm[i] for i in pick], 45, seed=1604)
 
 
-@pytest.mark.parametrize("mask", [0xFF0, 0xAB5])
+@pytest.mark.parametrize("mask", [0xFF0, 0xEB5])
 def test_decode_device_8p4_large_batch(ec, oracle, torch_cuda, mask):
     """More than 131,072 stripes of 8+4: the 4-wave-block instantiation the
     launcher picks for large full decodes (ec_kernels.hip launch_combine_k)."""
