@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ec_gf8_prog.h"
+
 namespace ecgf {
 
 typedef uint32_t u32;
@@ -52,12 +54,13 @@ __device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c)
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-/* out[p] = base[p] ^ (C * src)[p], folded into XOR3 chains.  `out` may alias
- * `base` (each element of base is read before the same element is written),
- * but must not alias `src`. */
+/* out[p] = base[p] ^ (C * src)[p] with each plane's own XOR3 chain and no
+ * sharing between planes: 18.07 instructions per multiply-accumulate on
+ * average (round-1 form, kept for A/B runs in tools/kbench).  `out` may
+ * alias `base`, but must not alias `src`. */
 template <u32 C, int W>
-__device__ __forceinline__ void mul_xor(u32 (&out)[8][W], const u32 (&base)[8][W],
-                                        const u32 (&src)[8][W])
+__device__ __forceinline__ void mul_xor_naive(u32 (&out)[8][W], const u32 (&base)[8][W],
+                                              const u32 (&src)[8][W])
 {
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
@@ -85,12 +88,63 @@ __device__ __forceinline__ void mul_xor(u32 (&out)[8][W], const u32 (&base)[8][W
     }
 }
 
+/* acc ^= C * x by the searched program of ec_gf8_prog.h (tools/gen): shared
+ * temporaries across the 8 output planes, 12.85 v_bitop3/v_xor per
+ * multiply-accumulate per dword on average (the reference's own searched
+ * programs, ec-gf8.c, average 12.8 XOR2 for the multiply alone, before the
+ * 8 accumulating XORs: ec-implementation.md:516-519). */
+template <u32 C>
+struct Prog;
+
+#define ECGF_X(b) x[b][w]
+#define ECGF_TV(j) t##j
+#define ECGF_T2(j, s1, s2) const u32 t##j = (s1) ^ (s2);
+#define ECGF_T3(j, s1, s2, s3) const u32 t##j = xor3(s1, s2, s3);
+#define ECGF_A1(p, s1) a[p][w] ^= (s1);
+#define ECGF_A2(p, s1, s2) a[p][w] = xor3(a[p][w], s1, s2);
+#define ECGF_DEF(c)                                                            \
+    template <>                                                                \
+    struct Prog<c> {                                                           \
+        template <int W>                                                       \
+        __device__ __forceinline__ static void run(u32 (&a)[8][W],            \
+                                                   const u32 (&x)[8][W])      \
+        {                                                                      \
+            _Pragma("unroll") for (int w = 0; w < W; ++w) { ECGF_PROG_##c }   \
+        }                                                                      \
+    };
+ECGF_FOR_EACH(ECGF_DEF)
+#undef ECGF_DEF
+#undef ECGF_A2
+#undef ECGF_A1
+#undef ECGF_T3
+#undef ECGF_T2
+#undef ECGF_TV
+#undef ECGF_X
+
+/* out[p] = base[p] ^ (C * src)[p].  `out` may alias `base`, but must not
+ * alias `src`. */
+template <u32 C, int W, bool CSE = true>
+__device__ __forceinline__ void mul_xor(u32 (&out)[8][W], const u32 (&base)[8][W],
+                                        const u32 (&src)[8][W])
+{
+    if constexpr (!CSE) {
+        mul_xor_naive<C, W>(out, base, src);
+    } else {
+#pragma unroll
+        for (int p = 0; p < 8; ++p)
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+                out[p][w] = base[p][w];
+        Prog<C>::template run<W>(out, src);
+    }
+}
+
 /* Horner step acc = C*acc ^ d  (ec-code-c.c:11647-11657 inner statement). */
-template <u32 C, int W>
+template <u32 C, int W, bool CSE = true>
 __device__ __forceinline__ void horner(u32 (&acc)[8][W], const u32 (&d)[8][W])
 {
     u32 t[8][W];
-    mul_xor<C, W>(t, d, acc);
+    mul_xor<C, W, CSE>(t, d, acc);
 #pragma unroll
     for (int p = 0; p < 8; ++p)
 #pragma unroll
@@ -102,13 +156,13 @@ __device__ __forceinline__ void horner(u32 (&acc)[8][W], const u32 (&d)[8][W])
  * a scalar compare tree (no divergence: c lives in an SGPR); c == 0 adds
  * nothing, matching the zero-skipping of ec_code_c_interleaved
  * (ec-code-c.c:11666-11676). */
-template <int W>
+template <int W, bool CSE = true>
 __device__ __forceinline__ void mul_xor_rt(u32 c, u32 (&acc)[8][W], const u32 (&x)[8][W])
 {
     switch (c) {
 #define ECGF_CASE(n)                                                           \
     case n:                                                                    \
-        mul_xor<n, W>(acc, acc, x);                                            \
+        mul_xor<n, W, CSE>(acc, acc, x);                                       \
         break;
 #define ECGF_CASE16(h)                                                         \
     ECGF_CASE(h * 16 + 0) ECGF_CASE(h * 16 + 1) ECGF_CASE(h * 16 + 2)          \

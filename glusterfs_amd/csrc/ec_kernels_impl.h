@@ -134,7 +134,7 @@ struct FragPtrs {
 };
 
 /* Row I (evaluation point v = I + 1) of the reversed Vandermonde matrix. */
-template <int K, int W, int I>
+template <int K, int W, int I, bool CSE = true>
 __device__ __forceinline__ void encode_row_acc(const u32 (&x)[K][8][W], u32 (&acc)[8][W])
 {
     constexpr u32 v = I + 1;
@@ -161,27 +161,29 @@ __device__ __forceinline__ void encode_row_acc(const u32 (&x)[K][8][W], u32 (&ac
                 acc[b][w] = x[0][b][w];
 #pragma unroll
         for (int j = 1; j < K; ++j)
-            ecgf::horner<v, W>(acc, x[j]);
+            ecgf::horner<v, W, CSE>(acc, x[j]);
     }
 }
 
-template <int K, int W, int I, bool NTS>
+template <int K, int W, int I, bool NTS, bool CSE = true>
 __device__ __forceinline__ void encode_row(const u32 (&x)[K][8][W], uint8_t *dst)
 {
     u32 acc[8][W];
-    encode_row_acc<K, W, I>(x, acc);
+    encode_row_acc<K, W, I, CSE>(x, acc);
     store_chunk<W, NTS>(dst, acc);
 }
 
-template <int K, int W, bool NTS, int... I>
+template <int K, int W, bool NTS, bool CSE, int... I>
 __device__ __forceinline__ void encode_rows(std::integer_sequence<int, I...>,
                                             const u32 (&x)[K][8][W], const FragPtrs &out,
                                             uint64_t off)
 {
-    (encode_row<K, W, I, NTS>(x, out.p[I] + off), ...);
+    (encode_row<K, W, I, NTS, CSE>(x, out.p[I] + off), ...);
 }
 
-template <int K, int N, int W, bool NTS>
+/* CSE: multiply by the searched programs of ec_gf8_prog.h (false: the
+ * round-1 per-plane trees, for A/B runs) */
+template <int K, int N, int W, bool NTS, bool CSE = true>
 __global__ __launch_bounds__(kBlock) void ec_encode_vander(const uint8_t *__restrict__ in,
                                                            const FragPtrs out,
                                                            uint64_t nstripes)
@@ -199,8 +201,8 @@ __global__ __launch_bounds__(kBlock) void ec_encode_vander(const uint8_t *__rest
     for (int j = 0; j < K; ++j)
         load_chunk<W>(s + j * ECD_CHUNK, x[j]);
 
-    encode_rows<K, W, NTS>(std::make_integer_sequence<int, N>{}, x, out,
-                           stripe * (uint64_t)ECD_CHUNK + colb);
+    encode_rows<K, W, NTS, CSE>(std::make_integer_sequence<int, N>{}, x, out,
+                                stripe * (uint64_t)ECD_CHUNK + colb);
 }
 
 template <int W>
@@ -406,7 +408,8 @@ __device__ __forceinline__ u32 tile_pattern(const CombineArgs &a, uint64_t t0)
  * one lane address serves all 8 planes of an input (ds_read2st64_b64 with
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
-template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false>
+template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
+          bool CSE = true>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -476,7 +479,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 #pragma unroll
             for (int b = 0; b < 8; ++b)
                 load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
-            ecgf::mul_xor_rt<CW>(c, acc, y);
+            ecgf::mul_xor_rt<CW, CSE>(c, acc, y);
         }
         const uint64_t ost = t0 + s;
         if (ost < a.nstripes)
@@ -765,8 +768,8 @@ __global__ __launch_bounds__(kBlock) void ec_encode_vander_rmw(const uint8_t *__
             for (int b = 0; b < 8; ++b)
                 load_plane_unaligned<W>(s + j * ECD_CHUNK + b * 64, x[j][b]);
     }
-    encode_rows<K, W, false>(std::make_integer_sequence<int, N>{}, x, out,
-                             stripe * (uint64_t)ECD_CHUNK + colb);
+    encode_rows<K, W, false, true>(std::make_integer_sequence<int, N>{}, x, out,
+                                   stripe * (uint64_t)ECD_CHUNK + colb);
 }
 
 } // namespace ecdev

@@ -308,26 +308,21 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
                         }, out, ob});
     };
     /* (GLDS / PF / register staging were measured here in r01a-c and
-     * removed; the shipped kernel stages by LDS-DMA into a plane-major tile) */
+     * removed; the shipped kernel stages by LDS-DMA into a plane-major tile.
+     * r02: the searched multiply programs of ec_gf8_prog.h ("CSE", the
+     * default) against the round-1 per-plane trees ("naive"); the bit-pair
+     * candidate kb_combine_bp lost in r01 and is no longer timed) */
     add("TS1 NW4 NTS", ec_combine<K, 1, 4, false, true>, 1, 4);
+    add("TS1 NW4 NTS naive", ec_combine<K, 1, 4, false, true, 2, false, false>, 1, 4);
     add("TS1 NW8 NTS", ec_combine<K, 1, 8, false, true>, 1, 8);
+    add("TS1 NW8 NTS naive", ec_combine<K, 1, 8, false, true, 2, false, false>, 1, 8);
     add("TS1 NW16 NTS", ec_combine<K, 1, 16, false, true>, 1, 16);
-    add("BP R4 NW8 NTS", kb_combine_bp<K, 8, 4, true>, 1, 8);
-    add("BP R2 NW16 NTS", kb_combine_bp<K, 16, 2, true>, 1, 16);
-    add("BP R2 NW8 NTS", kb_combine_bp<K, 8, 2, true>, 1, 8);
-    add("BP R1 NW16 NTS", kb_combine_bp<K, 16, 1, true>, 1, 16);
-    if (K <= 4)
-        add("TS2 NW4", ec_combine<K, 2, 4, false, false>, 2, 4);
-    if constexpr (K <= 8) {
-        add("TS2 NW8 NTS", ec_combine<K, 2, 8, false, true>, 2, 8);
-        add("TS2 NW16 NTS", ec_combine<K, 2, 16, false, true>, 2, 16);
-    }
-    if constexpr (K <= 4)
-        add("TS4 NW16 NTS", ec_combine<K, 4, 16, false, true>, 4, 16);
-    add("TS1 NW8 NTS CW1", ec_combine<K, 1, 8, false, true, 1>, 1, 8);
+    add("TS1 NW16 NTS naive", ec_combine<K, 1, 16, false, true, 2, false, false>, 1, 16);
     add("TS1 NW16 NTS CW1", ec_combine<K, 1, 16, false, true, 1>, 1, 16);
-    add("TS1 NW4", ec_combine<K, 1, 4, false, false>, 1, 4);
-    add("TS1 NW8", ec_combine<K, 1, 8, false, false>, 1, 8);
+    if constexpr (K <= 8) {   /* CW = 4: 16 stripes per item, 16-stripe tiles */
+        add("TS2 NW8 NTS CW4", ec_combine<K, 2, 8, false, true, 4>, 2, 8);
+        add("TS2 NW16 NTS CW4", ec_combine<K, 2, 16, false, true, 4>, 2, 16);
+    }
 }
 
 template <int K, int N, typename KF>
@@ -446,6 +441,7 @@ int main(int argc, char **argv)
                          }, bufB, (size_t)nst * RW * ECD_CHUNK});
         };
         addh("heal NW4 NTS", ec_combine<K, 1, 4, false, true>, 4);
+        addh("heal NW4 NTS naive", ec_combine<K, 1, 4, false, true, 2, false, false>, 4);
         addh("heal NW8 NTS", ec_combine<K, 1, 8, false, true>, 8);
         addh("heal NW16 NTS", ec_combine<K, 1, 16, false, true>, 16);
         run_group("heal 8+4 (regenerate 4 rows)", v, rounds, iters, s);
@@ -516,11 +512,12 @@ int main(int argc, char **argv)
                          }, bufB, (size_t)nst * K * ECD_CHUNK});
         };
         addm("mixed TS1 NW4 NTS", ec_combine<K, 1, 4, true, true>, 4);
+        addm("mixed TS1 NW8 NTS naive", ec_combine<K, 1, 8, true, true, 2, false, false>, 8);
         addm("mixed TS1 NW8 NTS", ec_combine<K, 1, 8, true, true>, 8);
         addm("mixed TS1 NW16 NTS", ec_combine<K, 1, 16, true, true>, 16);
         run_group("decode 8+4 mixed (16 patterns, 1024-stripe groups)", v, rounds, iters, s);
     }
-    if (getenv("KB_ENCODE")) {   /* encode 4+2, 8+4, 16+4 */
+    if (!getenv("KB_NO_ENCODE")) {   /* encode 4+2, 8+4, 16+4: shipped W/NTS, CSE vs naive */
         auto frag_ptrs = [&](uint64_t nst, int n) {
             FragPtrs f;
             for (int i = 0; i < n; ++i)
@@ -530,23 +527,24 @@ int main(int argc, char **argv)
         std::vector<Variant> v;
         uint64_t nst = user / (4 * ECD_CHUNK);
         FragPtrs f = frag_ptrs(nst, 6);
-        add_encode_w<4, 6>(v, "enc 4+2 W1", nst, bufA, f, ec_encode_vander<4, 6, 1, false>, 1);
         add_encode_w<4, 6>(v, "enc 4+2 W2", nst, bufA, f, ec_encode_vander<4, 6, 2, false>, 2);
-        add_encode_w<4, 6>(v, "enc 4+2 W4", nst, bufA, f, ec_encode_vander<4, 6, 4, false>, 4);
-        add_encode_w<4, 6>(v, "enc 4+2 W2 NTS", nst, bufA, f, ec_encode_vander<4, 6, 2, true>, 2);
+        add_encode_w<4, 6>(v, "enc 4+2 W2 naive", nst, bufA, f,
+                           ec_encode_vander<4, 6, 2, false, false>, 2);
         run_group("encode 4+2", v, rounds, iters, s);
         v.clear();
         nst = user / (8 * ECD_CHUNK);
         f = frag_ptrs(nst, 12);
-        add_encode_w<8, 12>(v, "enc 8+4 W1", nst, bufA, f, ec_encode_vander<8, 12, 1, false>, 1);
-        add_encode_w<8, 12>(v, "enc 8+4 W2", nst, bufA, f, ec_encode_vander<8, 12, 2, false>, 2);
         add_encode_w<8, 12>(v, "enc 8+4 W1 NTS", nst, bufA, f, ec_encode_vander<8, 12, 1, true>, 1);
+        add_encode_w<8, 12>(v, "enc 8+4 W1 NTS naive", nst, bufA, f,
+                            ec_encode_vander<8, 12, 1, true, false>, 1);
+        add_encode_w<8, 12>(v, "enc 8+4 W2 NTS", nst, bufA, f, ec_encode_vander<8, 12, 2, true>, 2);
         run_group("encode 8+4", v, rounds, iters, s);
         v.clear();
         nst = user / (16 * ECD_CHUNK);
         f = frag_ptrs(nst, 20);
-        add_encode_w<16, 20>(v, "enc 16+4 W1", nst, bufA, f, ec_encode_vander<16, 20, 1, false>, 1);
         add_encode_w<16, 20>(v, "enc 16+4 W1 NTS", nst, bufA, f, ec_encode_vander<16, 20, 1, true>, 1);
+        add_encode_w<16, 20>(v, "enc 16+4 W1 NTS naive", nst, bufA, f,
+                             ec_encode_vander<16, 20, 1, true, false>, 1);
         run_group("encode 16+4", v, rounds, iters, s);
     }
     return 0;
