@@ -461,12 +461,12 @@ def test_decode_mixed_null_fragment_rejected(ec, torch_cuda):
     torch = torch_cuda
     k, n, nst = 4, 6, 64
     frags = [rand_bytes(CHUNK * nst, f) for f in range(n)]
-    frags[2] = None                                  # brick 2 absent
+    frags[0] = None                                  # brick 0 absent
     out = np.zeros(CHUNK * k * nst, np.uint8)
     with ec.ECMatrixList(k, n) as L:
-        L.decode_mixed(nst, 8, [0x3C] * 8, frags, out)          # 0x3C skips 0,1 only
+        L.decode_mixed(nst, 8, [0x3C] * 8, frags, out)          # 0x3C reads bricks 2-5
         with pytest.raises(OSError) as ei:
-            L.decode_mixed(nst, 8, [0x3C, 0x0F] * 4, frags, out)  # 0x0F reads brick 2
+            L.decode_mixed(nst, 8, [0x3C, 0x0F] * 4, frags, out)  # 0x0F reads brick 0
         assert ei.value.errno == errno.EINVAL
         dfr = [None if f is None else torch.from_numpy(f).cuda() for f in frags]
         dout = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
