@@ -13,7 +13,9 @@ from .ec_method import (  # noqa: F401
     gf_div,
     gf_mul,
     host_registered,
+    inject_device_faults,
     inverse_matrix,
     mask_rows,
+    stats,
     sync_device,
 )

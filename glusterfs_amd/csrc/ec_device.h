@@ -46,8 +46,8 @@ typedef struct ecd_combine_desc {
     uint8_t pat[ECD_MAX_PAT_BYTES];
 } ecd_combine_desc_t;
 
-/* Number of usable gfx950 devices (0 when none: callers fail, there is no
- * CPU fallback anywhere in the product path). */
+/* Number of usable gfx950 devices (0 when none: the host layer then codes
+ * with its CPU engine, ec_cpu.h). */
 int ecd_device_count(void);
 const char *ecd_last_error(void);
 
@@ -101,6 +101,14 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes,
                     uint32_t nfrags, const void *const *frags, void *out,
                     void *const *outs, uint32_t npatterns, const uint8_t *pats,
                     const uint8_t *group_pattern, uint32_t group_shift);
+
+/* 1 when every host-buffer device has at least `limit` bytes in flight
+ * (or no device exists): the caller should code on its own CPU thread. */
+int ecd_host_busy(uint64_t limit);
+
+/* Test hook: the next n host-buffer submissions fail with -EIO before
+ * touching a device (exercises the CPU fallback). */
+void ecd_inject_faults(uint32_t n);
 
 /* Pointer classification: index of the (gfx950) device owning device
  * memory `p`, or -1 for host memory (pageable or pinned). */

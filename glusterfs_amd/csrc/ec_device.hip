@@ -701,17 +701,40 @@ int pick_device(uint64_t bytes)
     return best;
 }
 
+/* Test hook (ec_method_inject_device_faults): the next N host-buffer
+ * submissions fail with -EIO before touching a device. */
+std::atomic<uint32_t> g_inject_faults{0};
+
+bool take_injected_fault()
+{
+    uint32_t v = g_inject_faults.load();
+    while (v > 0 && !g_inject_faults.compare_exchange_weak(v, v - 1))
+        ;
+    if (v > 0) {
+        std::lock_guard<std::mutex> g(g_err_mu);
+        g_err = "injected device fault (ec_method_inject_device_faults)";
+        return true;
+    }
+    return false;
+}
+
 /* Run fn(dev, s0, s1) over a stripe-range partition; `align` keeps every
- * range boundary a multiple of it (pattern groups). */
+ * range boundary a multiple of it (pattern groups).  Bytes in flight are
+ * tracked per device for placement and for the CPU crossover
+ * (ecd_host_busy). */
 template <typename F>
 int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
 {
     if (g_ndev == 0)
         return -ENODEV;
+    if (take_injected_fault())
+        return -EIO;
     if (ndev <= 0 || ndev > g_nhost)
         ndev = g_nhost;
-    if (ndev > 1 && bytes < split_min_bytes()) {
-        const int d = pick_device(bytes);
+    if (ndev == 1 || bytes < split_min_bytes()) {
+        const int d = ndev == 1 ? g_host_devs[0] : pick_device(bytes);
+        if (ndev == 1)
+            g_inflight[d].fetch_add(bytes);
         const int rc = fn(d, 0, nstripes);
         g_inflight[d].fetch_sub(bytes);
         return rc;
@@ -720,11 +743,14 @@ int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
     if ((uint64_t)ndev > units)
         ndev = (int)std::max<uint64_t>(1, units);
     std::vector<int> rcs(ndev, 0);
+    std::vector<uint64_t> share(ndev, 0);
     std::vector<std::thread> th;
     for (int d = 0; d < ndev; ++d) {
         const uint64_t s0 = std::min(nstripes, units * d / ndev * align);
         const uint64_t s1 = std::min(nstripes, units * (d + 1) / ndev * align);
         const int dev = g_host_devs[d];
+        share[d] = nstripes ? bytes / nstripes * (s1 - s0) : 0;
+        g_inflight[dev].fetch_add(share[d]);
         if (d == ndev - 1)
             rcs[d] = fn(dev, s0, s1);
         else
@@ -732,6 +758,8 @@ int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
     }
     for (auto &t : th)
         t.join();
+    for (int d = 0; d < ndev; ++d)
+        g_inflight[g_host_devs[d]].fetch_sub(share[d]);
     for (int rc : rcs)
         if (rc)
             return rc;
@@ -916,6 +944,21 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, uint
         j.s1 = s1;
         return run_decode_dev(d, j);
     });
+}
+
+int ecd_host_busy(uint64_t limit)
+{
+    if (ecd_device_count() == 0)
+        return 1;
+    for (int i = 0; i < g_nhost; ++i)
+        if (g_inflight[g_host_devs[i]].load() < limit)
+            return 0;
+    return 1;
+}
+
+void ecd_inject_faults(uint32_t n)
+{
+    g_inject_faults.store(n);
 }
 
 int ecd_ptr_device(const void *p)

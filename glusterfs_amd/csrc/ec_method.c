@@ -7,8 +7,12 @@
  * (ec-method.c:22-36), the per-mask inverse (ec-method.c:38-72) and the LRU
  * cache of inverses keyed by brick mask (ec-method.c:134-256).  The per-byte
  * work -- the reference's row kernels called from ec-method.c:401-407 and
- * :422-428 -- is handed to the gfx950 kernels through ec_device.h.  There is
- * no CPU coding path: without a device, ec_method_init() fails.
+ * :422-428 -- goes to the gfx950 kernels through ec_device.h, or to the CPU
+ * engine of ec_cpu.h: on nodes without a gfx950 GPU, for cpu-extensions =
+ * none / x64 / sse / avx, for host-buffer calls below the crossover or when
+ * every GPU is saturated, and as the fallback when a device submission for
+ * host buffers fails (the reference coder cannot fail: ec-method.c:393-408,
+ * ec-code.c:1007-1013).
  *
  * Storage contract: only the 120 bytes of the caller's ec_matrix_list_t are
  * used (ec-types.h:549-562, embedded by value in ec_t at ec-types.h:677):
@@ -27,6 +31,7 @@
 #include <string.h>
 
 #include "../../include/ec_method.h"
+#include "ec_cpu.h"
 #include "ec_device.h"
 
 _Static_assert(sizeof(ec_matrix_list_t) == 120, "ec_matrix_list_t must stay 120 bytes");
@@ -201,12 +206,103 @@ typedef struct ecm_matrix {
     uint32_t inv[ECM_MAX_K * ECM_MAX_K];
 } ecm_matrix_t;
 
+enum { ECM_ENGINE_GPU = 0, ECM_ENGINE_CPU = 1 };
+
 typedef struct {
     uint32_t k, n;
     uint32_t enc[ECM_MAX_N * ECM_MAX_K];
     uint8_t enc_pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K]; /* src[k] + n x k */
     char gen[16];
+    int engine; /* ECM_ENGINE_GPU: gfx950 + CPU crossover / fallback */
+    int isa;    /* CPU engine ISA level (ec_cpu.h)                   */
+    char engine_name[48];
 } ecm_ctx_t;
+
+/* ------------------------------------------------------ engine counters */
+
+static uint64_t ecm_stat_gpu, ecm_stat_cpu, ecm_stat_fallback;
+
+static void
+stat_add(uint64_t *c)
+{
+    __atomic_fetch_add(c, 1, __ATOMIC_RELAXED);
+}
+
+void
+ec_method_get_stats(ec_method_stats_t *st)
+{
+    if (!st)
+        return;
+    st->gpu_calls = __atomic_load_n(&ecm_stat_gpu, __ATOMIC_RELAXED);
+    st->cpu_calls = __atomic_load_n(&ecm_stat_cpu, __ATOMIC_RELAXED);
+    st->cpu_fallbacks = __atomic_load_n(&ecm_stat_fallback, __ATOMIC_RELAXED);
+}
+
+void
+ec_method_inject_device_faults(uint32_t count)
+{
+    ecd_inject_faults(count);
+}
+
+/* Host-buffer crossover.  GlusterFS codes one fop per
+ * call: 128 KiB FUSE writes (fuse-bridge.c:5179) up to 4 MiB heal blocks
+ * (ec-heal.c:2063-2068), on several threads at once.  A call whose bytes
+ * (read + written) are below EC_CPU_BELOW_KB runs on the calling thread, as
+ * a PCIe round trip costs more; so does a call that finds every GPU with
+ * EC_GPU_INFLIGHT_MB or more of host-buffer work in flight, so concurrent
+ * callers use the CPU and the GPUs together.  Defaults from the smallcalls
+ * measurements on MI355X. */
+static uint64_t
+env_u64(const char *name, uint64_t dflt)
+{
+    const char *e = getenv(name);
+    char *end = NULL;
+    unsigned long long v;
+
+    if (!e || !*e)
+        return dflt;
+    v = strtoull(e, &end, 10);
+    return (end && *end == 0) ? (uint64_t)v : dflt;
+}
+
+static uint64_t ecm_cpu_below, ecm_gpu_inflight;
+static pthread_once_t ecm_xover_once = PTHREAD_ONCE_INIT;
+
+static void
+xover_init(void)
+{
+    ecm_cpu_below = env_u64("EC_CPU_BELOW_KB", 1024) << 10;
+    ecm_gpu_inflight = env_u64("EC_GPU_INFLIGHT_MB", 64) << 20;
+}
+
+/* 1: code this host-buffer call on the CPU engine */
+static int
+route_cpu(const ecm_ctx_t *ctx, uint64_t bytes)
+{
+    if (ctx->engine == ECM_ENGINE_CPU)
+        return 1;
+    pthread_once(&ecm_xover_once, xover_init);
+    if (bytes < ecm_cpu_below)
+        return 1;
+    return ecd_host_busy(ecm_gpu_inflight);
+}
+
+/* A failed device submission for host buffers: log once, count, and let
+ * the caller redo the call on the CPU engine (-EINVAL is an argument error
+ * the CPU would reject as well, and is returned). */
+static int
+gpu_failed(int rc)
+{
+    static int logged;
+
+    if (rc == 0 || rc == -EINVAL || rc == -E2BIG)
+        return 0;
+    stat_add(&ecm_stat_fallback);
+    if (!__atomic_exchange_n(&logged, 1, __ATOMIC_RELAXED))
+        ecm_log("device submission failed (%d: %s); coding on the CPU engine", rc,
+                ecd_last_error());
+    return 1;
+}
 
 #define CTX(list) ((ecm_ctx_t *)(list)->code)
 #define LRU_HEAD(list) ((ecm_matrix_t *)(void *)(list)->lru)
@@ -505,8 +601,46 @@ ec_method_host_unregister(void *p)
     return ecd_host_unregister(p);
 }
 
-static const char *const ecm_known_gens[] = {"none", "auto", "x64", "sse", "avx", "hip",
-                                             NULL};
+/* disperse.cpu-extensions (ec.c:1786-1794) -> engine.  The reference maps
+ * none to portable C and x64 / sse / avx to its JIT back ends, auto to the
+ * best of them (ec-code.c:59-69, 977-1060).  Here auto (and hip) select the
+ * gfx950 engine when a device is visible -- with the CPU engine beside it
+ * for small calls and as the fallback -- and the CPU engine otherwise; none,
+ * x64 and sse select the CPU engine at the base x86-64 level, avx the best
+ * AVX level of this CPU (library extensions, not in ec.c's option table:
+ * avx2 / avx512 pin that level, for tests and tuning).  Unknown values warn
+ * and act as auto, as the reference's fall back to C with a warning
+ * (ec-code.c:1007-1013). */
+static void
+pick_engine(ecm_ctx_t *ctx, const char *gen)
+{
+    int isa_best = ecc_isa_max(), want_gpu = 1;
+
+    ctx->isa = isa_best;
+    if (gen && (!strcmp(gen, "none") || !strcmp(gen, "x64") || !strcmp(gen, "sse"))) {
+        want_gpu = 0;
+        ctx->isa = ECC_ISA_BASE;
+    } else if (gen && !strcmp(gen, "avx")) {
+        want_gpu = 0;
+    } else if (gen && !strcmp(gen, "avx2")) {
+        want_gpu = 0;
+        ctx->isa = isa_best < ECC_ISA_AVX2 ? isa_best : ECC_ISA_AVX2;
+    } else if (gen && !strcmp(gen, "avx512")) {
+        want_gpu = 0;
+    } else if (gen && strcmp(gen, "auto") && strcmp(gen, "hip")) {
+        ecm_log("unknown cpu-extensions value '%s', using 'auto'", gen);
+    }
+    if (want_gpu && ecd_device_count() == 0) {
+        ecm_log("no MI355X (gfx950) device visible (%s): CPU engine", ecd_last_error());
+        want_gpu = 0;
+    }
+    ctx->engine = want_gpu ? ECM_ENGINE_GPU : ECM_ENGINE_CPU;
+    if (want_gpu)
+        snprintf(ctx->engine_name, sizeof(ctx->engine_name), "gfx950 x%d + cpu/%s",
+                 ecd_device_count(), ecc_isa_name(ctx->isa));
+    else
+        snprintf(ctx->engine_name, sizeof(ctx->engine_name), "cpu/%s", ecc_isa_name(ctx->isa));
+}
 
 int32_t
 ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t rows,
@@ -514,7 +648,6 @@ ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t 
 {
     ecm_ctx_t *ctx;
     uint32_t i;
-    int known = 0;
 
     (void)xl;
     if (!list)
@@ -522,15 +655,6 @@ ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t 
     memset(list, 0, sizeof(*list));
     if (columns < 1 || columns > ECM_MAX_K || rows < columns || rows > ECM_MAX_N)
         return -EINVAL;
-    if (ecd_device_count() == 0) {
-        ecm_log("no MI355X (gfx950) device: %s; refusing to start (no CPU path)",
-                ecd_last_error());
-        return -ENODEV;
-    }
-    for (i = 0; gen && ecm_known_gens[i]; i++)
-        known |= strcmp(gen, ecm_known_gens[i]) == 0;
-    if (gen && !known)
-        ecm_log("unknown cpu-extensions value '%s', using the gfx950 engine", gen);
 
     ctx = (ecm_ctx_t *)calloc(1, sizeof(*ctx));
     list->objects = (void **)calloc(max ? max : 1, sizeof(void *));
@@ -543,6 +667,7 @@ ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t 
     ctx->k = columns;
     ctx->n = rows;
     snprintf(ctx->gen, sizeof(ctx->gen), "%s", gen ? gen : "auto");
+    pick_engine(ctx, gen);
     ec_method_encode_matrix(columns, rows, ctx->enc);
     {
         uint8_t src[ECM_MAX_K];
@@ -561,10 +686,20 @@ ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t 
     list->encode = ctx->enc;
     lru_init(list);
     pthread_mutex_init(&list->lock, NULL);
-    ecm_log("disperse %u+%u on %d MI355X device(s) (cpu-extensions=%s -> gfx950 %s)",
-            columns, rows - columns, ecd_device_count(), ctx->gen,
-            ecd_has_vander(columns, rows) ? "specialised encoder" : "generic encoder");
+    ecm_log("disperse %u+%u: %s engine (cpu-extensions=%s%s)", columns, rows - columns,
+            ctx->engine_name, ctx->gen,
+            ctx->engine == ECM_ENGINE_GPU
+                ? (ecd_has_vander(columns, rows) ? ", specialised encoder" : ", generic encoder")
+                : "");
     return 0;
+}
+
+const char *
+ec_method_engine(const ec_matrix_list_t *list)
+{
+    const ecm_ctx_t *ctx = list ? (const ecm_ctx_t *)list->code : NULL;
+
+    return ctx ? ctx->engine_name : "";
 }
 
 void
@@ -621,27 +756,95 @@ popcount_mask(uintptr_t m)
     return c;
 }
 
+/* Host-buffer encode: the GPU pipeline, or the CPU engine (crossover,
+ * CPU-only volumes, and the fallback when the device submission fails). */
+static int
+host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
+{
+    const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n);
+    int rc;
+
+    if (!route_cpu(ctx, bytes)) {
+        rc = ecd_encode_host(0, ctx->k, ctx->n, nstripes, in, out, ctx->enc_pat);
+        if (!gpu_failed(rc)) {
+            if (rc == 0)
+                stat_add(&ecm_stat_gpu);
+            return rc;
+        }
+    }
+    ecc_encode(ctx->isa, ctx->k, ctx->n, nstripes, (const uint8_t *)in, (uint8_t *const *)out);
+    stat_add(&ecm_stat_cpu);
+    return 0;
+}
+
+/* Host-buffer combination (decode, mixed decode, heal): the GPU pipeline or
+ * the CPU engine, same arguments as ecd_decode_host. */
+static int
+host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32_t nfrags,
+            const void *const *frags, void *out, void *const *outs, uint32_t npat,
+            const uint8_t *pats, const uint8_t *gp, uint32_t shift)
+{
+    const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (k + rows);
+    ecd_combine_desc_t d;
+    uint32_t f, r;
+    int rc;
+
+    if (!route_cpu(ctx, bytes)) {
+        rc = ecd_decode_host(0, k, rows, nstripes, nfrags, frags, out, outs, npat, pats, gp,
+                             shift);
+        if (!gpu_failed(rc)) {
+            if (rc == 0)
+                stat_add(&ecm_stat_gpu);
+            return rc;
+        }
+    }
+    memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
+    d.k = k;
+    d.rows = rows;
+    d.nstripes = nstripes;
+    d.in_stride = EC_METHOD_CHUNK_SIZE;
+    for (f = 0; f < nfrags; f++)
+        d.in_base[f] = frags[f];
+    if (outs) {
+        d.out_stride = EC_METHOD_CHUNK_SIZE;
+        for (r = 0; r < rows; r++)
+            d.out_base[r] = outs[r];
+    } else {
+        d.out_stride = (uint64_t)rows * EC_METHOD_CHUNK_SIZE;
+        for (r = 0; r < rows; r++)
+            d.out_base[r] = (uint8_t *)out + (uint64_t)r * EC_METHOD_CHUNK_SIZE;
+    }
+    d.npatterns = npat;
+    d.pat_bytes = k + rows * k;
+    d.pat_ext = pats;
+    d.group_pattern = gp;
+    d.group_shift = shift;
+    rc = ecc_combine(ctx->isa, &d);
+    if (rc == 0)
+        stat_add(&ecm_stat_cpu);
+    return rc;
+}
+
 static int
 encode_any(ec_matrix_list_t *list, uint64_t nstripes, const void *in, void *const *out)
 {
     ecm_ctx_t *ctx = CTX(list);
-    int dev;
     uint32_t i;
+    int dev;
 
     if (nstripes == 0)
         return 0;
+    for (i = 0; i < ctx->n; i++)
+        if (!out[i])
+            return -EINVAL;
     dev = ecd_ptr_device(in);
+    if (!bufs_on((const void *const *)out, ctx->n, dev))
+        return -EINVAL; /* mixed host/device buffers are not supported */
     if (dev >= 0) {
-        for (i = 0; i < ctx->n; i++)
-            if (ecd_ptr_device(out[i]) != dev)
-                return -EINVAL;
         int rc = ec_method_encode_device(list, dev, NULL, nstripes, in, out);
         return rc ? rc : ecd_sync(dev, NULL);
     }
-    for (i = 0; i < ctx->n; i++)
-        if (ecd_ptr_device(out[i]) >= 0)
-            return -EINVAL; /* mixed host/device buffers are not supported */
-    return ecd_encode_host(0, ctx->k, ctx->n, nstripes, in, out, ctx->enc_pat);
+    return host_encode(ctx, nstripes, in, out);
 }
 
 void
@@ -656,6 +859,9 @@ ec_method_encode(ec_matrix_list_t *list, uint64_t size, void *in, void **out)
                 (unsigned long long)size, list->stripe);
         abort();
     }
+    /* host buffers cannot fail here (a device error is redone on the CPU
+     * engine); what is left is a caller error or a fault of caller-provided
+     * device memory, which no fallback can read */
     rc = encode_any(list, size / list->stripe, in, out);
     if (rc != 0) {
         ecm_log("ec_method_encode failed (%d): %s", rc, ecd_last_error());
@@ -688,17 +894,16 @@ decode_any(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask, const uint
         return -EINVAL;
     if (nstripes == 0)
         return 0;
+    for (p = 0; p < k; p++)
+        if (!in[p])
+            return -EINVAL;
     dev = ecd_ptr_device(out);
+    if (!bufs_on(in, k, dev))
+        return -EINVAL;
     if (dev >= 0) {
-        for (p = 0; p < k; p++)
-            if (ecd_ptr_device(in[p]) != dev)
-                return -EINVAL;
         rc = ec_method_decode_device(list, dev, NULL, nstripes, mask, in, out);
         return rc ? rc : ecd_sync(dev, NULL);
     }
-    for (p = 0; p < k; p++)
-        if (ecd_ptr_device(in[p]) >= 0)
-            return -EINVAL;
     m = matrix_get(list, mask, rows);
     if (!m)
         return -ENOMEM;
@@ -706,7 +911,7 @@ decode_any(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask, const uint
         src[p] = (uint8_t)p;
     pack_pattern(pat, k, src, k, m->inv);
     matrix_put(list, m);
-    return ecd_decode_host(0, k, k, nstripes, k, in, out, NULL, 1, pat, NULL, 0);
+    return host_decode(CTX(list), k, k, nstripes, k, in, out, NULL, 1, pat, NULL, 0);
 }
 
 int32_t
@@ -813,9 +1018,11 @@ ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group
         }
         gp[g] = (uint8_t)u;
     }
+    if (rc == 0 && (!bufs_on(frags, list->rows, -1) || ecd_ptr_device(out) >= 0))
+        rc = -EINVAL; /* host entry point: device buffers go to _device */
     if (rc == 0)
-        rc = ecd_decode_host(0, k, k, nstripes, list->rows, frags, out, NULL, nu, pats, gp,
-                             shift);
+        rc = host_decode(CTX(list), k, k, nstripes, list->rows, frags, out, NULL, nu, pats, gp,
+                         shift);
     free(pats);
     free(gp);
     return rc;
@@ -888,8 +1095,8 @@ ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
     rc = heal_pattern(list, mask, rows, target_mask, pat, &nt);
     if (rc)
         return rc;
-    return ecd_decode_host(0, list->columns, nt, nstripes, list->columns, in, NULL, out, 1,
-                           pat, NULL, 0);
+    return host_decode(CTX(list), list->columns, nt, nstripes, list->columns, in, NULL, out, 1,
+                       pat, NULL, 0);
 }
 
 /* ------------------------------------------------- partial-stripe writes */
@@ -951,7 +1158,18 @@ ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iove
     }
     segp[ns] = ts;
     segl[ns++] = nst * S - b2;
-    return ecd_encode_host_gather(0, ctx->k, ctx->n, nst, ns, segp, segl, out, ctx->enc_pat);
+    if (!route_cpu(ctx, nst * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n))) {
+        c = ecd_encode_host_gather(0, ctx->k, ctx->n, nst, ns, segp, segl, out, ctx->enc_pat);
+        if (!gpu_failed(c)) {
+            if (c == 0)
+                stat_add(&ecm_stat_gpu);
+            return c;
+        }
+    }
+    c = ecc_encode_gather(ctx->isa, ctx->k, ctx->n, nst, ns, segp, segl, (uint8_t *const *)out);
+    if (c == 0)
+        stat_add(&ecm_stat_cpu);
+    return c;
 }
 
 int32_t

@@ -8,8 +8,9 @@ errno returns become ``OSError(errno)``; ``ec_method_encode`` mirrors the
 reference's ``void`` signature.
 
 Buffers can be numpy arrays, torch tensors (host or device), ctypes buffers or
-plain integer addresses.  There is no Python or CPU coding fallback: if the
-library is missing, importing this module raises.
+plain integer addresses.  All coding happens in the native library (gfx950
+kernels, or its C CPU engine for host buffers); there is no Python coding
+path: if the library is missing, importing this module raises.
 """
 import ctypes
 import errno
@@ -37,7 +38,8 @@ EXPORTS = (
     "ec_method_encode_matrix", "ec_method_inverse_matrix", "ec_method_gf_mul",
     "ec_method_gf_div", "ec_method_config_fill", "ec_method_config_pack",
     "ec_method_config_unpack", "ec_method_config_check", "ec_method_writev_encode",
-    "ec_method_writev_encode_device",
+    "ec_method_writev_encode_device", "ec_method_engine", "ec_method_get_stats",
+    "ec_method_inject_device_faults",
 )
 
 
@@ -73,6 +75,12 @@ def _nbytes(buf):
     if hasattr(buf, "numel"):
         return int(buf.numel() * buf.element_size())
     return len(buf)
+
+
+class Stats(ctypes.Structure):
+    """ec_method_stats_t: process-wide engine counters."""
+    _fields_ = [("gpu_calls", ctypes.c_uint64), ("cpu_calls", ctypes.c_uint64),
+                ("cpu_fallbacks", ctypes.c_uint64)]
 
 
 class Config(ctypes.Structure):
@@ -142,6 +150,9 @@ def _load():
         "ec_method_config_pack": (i32, [ctypes.POINTER(Config), vp]),
         "ec_method_config_unpack": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(Config)]),
         "ec_method_config_check": (i32, [u32, u32, ctypes.POINTER(Config)]),
+        "ec_method_engine": (ctypes.c_char_p, [P]),
+        "ec_method_get_stats": (None, [ctypes.POINTER(Stats)]),
+        "ec_method_inject_device_faults": (None, [u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -180,6 +191,18 @@ def _check(rc, what):
 
 def device_count():
     return lib.ec_method_device_count()
+
+
+def stats():
+    """Process-wide engine counters as a dict (ec_method_get_stats)."""
+    st = Stats()
+    lib.ec_method_get_stats(ctypes.byref(st))
+    return dict(gpu_calls=st.gpu_calls, cpu_calls=st.cpu_calls, cpu_fallbacks=st.cpu_fallbacks)
+
+
+def inject_device_faults(count):
+    """Test hook: the next `count` host-buffer device submissions fail."""
+    lib.ec_method_inject_device_faults(count)
 
 
 class PinnedArray:
@@ -273,6 +296,10 @@ class ECMatrixList:
         self._live = True
 
     # --- reference surface -------------------------------------------------
+    @property
+    def engine(self):
+        return (lib.ec_method_engine(ctypes.byref(self._list)) or b"").decode()
+
     @property
     def stripe(self):
         return self._list.stripe

@@ -10,8 +10,11 @@
  * ec-inode-read.c and ec-heal.c link against it unchanged.
  *
  * Data buffers may be host memory (pageable or pinned) or MI355X device
- * memory; host data crosses PCIe inside the call.  There is no CPU coding
- * path: without a gfx950 device ec_method_init() fails with -ENODEV.
+ * memory; host data crosses PCIe inside the call, or is coded on the calling
+ * thread by the library's CPU engine: on nodes without a gfx950 device, for
+ * cpu-extensions = none / x64 / sse / avx, for host calls below the
+ * CPU/GPU crossover or while every GPU is saturated, and as the fallback
+ * when a device submission fails (the reference coder never fails).
  */
 #ifndef EC_MI355X_EC_METHOD_H
 #define EC_MI355X_EC_METHOD_H
@@ -80,9 +83,13 @@ struct _ec_matrix_list {
 
 /* Replaces ec-method.c:299-353, called from ec.c:837.  columns = k data
  * fragments, rows = n bricks, max = decode matrix cache size (2n in ec.c),
- * gen = the disperse.cpu-extensions value (ec.c:1786-1794: none, auto, x64,
- * sse, avx) or "hip"; every value selects the gfx950 engine.  Returns 0,
- * -EINVAL (bad geometry), -ENOMEM, or -ENODEV (no MI355X visible). */
+ * gen = the disperse.cpu-extensions value (ec.c:1786-1794) or "hip":
+ *   auto, hip        gfx950 engine when a device is visible (with the CPU
+ *                    engine for small calls and as the fallback), else CPU
+ *   none, x64, sse   CPU engine, base x86-64 code
+ *   avx              CPU engine, best AVX level of the host (AVX2/AVX-512)
+ * Unknown values warn and act as auto (ec-code.c:1007-1013).  Returns 0,
+ * -EINVAL (bad geometry) or -ENOMEM. */
 int32_t ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns,
                        uint32_t rows, uint32_t max, const char *gen);
 
@@ -96,8 +103,10 @@ int32_t ec_method_update(xlator_t *xl, ec_matrix_list_t *list, const char *gen);
 /* Replaces ec-method.c:393-408 (ec-inode-write.c:2136).  size: user bytes,
  * a multiple of EC_METHOD_CHUNK_SIZE * k.  out[i] receives size/k bytes of
  * fragment i and, as in the reference, each out[i] is advanced by size/k.
- * The reference cannot fail; this one aborts with a diagnostic if the device
- * fails (use ec_method_encode_batch for an error code). */
+ * Like the reference it cannot fail on host buffers: a device error is redone
+ * by the CPU engine.  Invalid arguments, or a fault with caller-provided
+ * device buffers, abort with a diagnostic (ec_method_encode_batch returns an
+ * error code instead). */
 void ec_method_encode(ec_matrix_list_t *list, uint64_t size, void *in, void **out);
 
 /* Replaces ec-method.c:410-433 (ec-inode-read.c:1196).  size: bytes per
@@ -232,8 +241,25 @@ int32_t ec_method_config_check(uint32_t bricks, uint32_t redundancy,
  * Utilities.
  * --------------------------------------------------------------------- */
 
-/* Number of visible gfx950 devices (0 = the library cannot run). */
+/* Number of visible gfx950 devices (0 = CPU engine only). */
 int32_t ec_method_device_count(void);
+/* The engine a volume's coder runs ("gfx950 x8 + cpu/avx512", "cpu/avx2"...),
+ * as logged by ec_method_init (cf. ec-code.c:1048-1053). */
+const char *ec_method_engine(const ec_matrix_list_t *list);
+
+/* Process-wide engine counters: host-buffer calls coded on a GPU, calls
+ * coded by the CPU engine, and, among the latter, fallbacks after a failed
+ * device submission. */
+typedef struct {
+    uint64_t gpu_calls;
+    uint64_t cpu_calls;
+    uint64_t cpu_fallbacks;
+} ec_method_stats_t;
+void ec_method_get_stats(ec_method_stats_t *stats);
+/* Fault injection for tests (cf. debug/error-gen): the next `count`
+ * host-buffer device submissions fail with -EIO before touching a device,
+ * so the CPU fallback runs. */
+void ec_method_inject_device_faults(uint32_t count);
 /* Last device-layer error string (diagnostics). */
 const char *ec_method_last_error(void);
 /* Pinned, device-mapped host memory.  Host buffers in such memory (16-byte

@@ -1,7 +1,9 @@
 /* Compiled with plain gcc against include/ec_method.h and linked against
  * glusterfs_amd/lib/libec_mi355x.so, the way GlusterFS's ec xlator would
  * (INTEGRATION.md).  Checks the 120-byte ec_matrix_list_t layout of
- * ec-types.h:549-562 and exercises ec_method_init/encode/decode/fini. */
+ * ec-types.h:549-562 and exercises ec_method_init/encode/decode/fini:
+ * argv[1] = "gpu" requires the gfx950 engine, "cpu" the CPU engine (a node
+ * without GPU, or cpu-extensions=none). */
 #include <errno.h>
 #include <stddef.h>
 #include <stdio.h>
@@ -25,15 +27,21 @@ main(int argc, char **argv)
         printf("layout mismatch\n");
         return 2;
     }
-    rc = ec_method_init(NULL, &list, 4, 6, 12, "auto");
-    if (!expect_gpu) {
-        printf("init=%d\n", rc);
-        ec_method_fini(&list); /* must be safe after a failed init */
-        return rc == -ENODEV ? 0 : 3;
+    rc = ec_method_init(NULL, &list, 8, 4, 8, "auto"); /* k > n: -EINVAL */
+    ec_method_fini(&list);                              /* safe after a failed init */
+    if (rc != -EINVAL) {
+        printf("bad geometry accepted: %d\n", rc);
+        return 3;
     }
+    rc = ec_method_init(NULL, &list, 4, 6, 12, expect_gpu ? "auto" : "none");
     if (rc != 0) {
         printf("init failed %d\n", rc);
         return 4;
+    }
+    printf("engine %s\n", ec_method_engine(&list));
+    if (expect_gpu != (strncmp(ec_method_engine(&list), "gfx950", 6) == 0)) {
+        printf("wrong engine\n");
+        return 7;
     }
     {
         enum { NST = 100, K = 4, N = 6 };

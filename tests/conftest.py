@@ -19,3 +19,12 @@ def oracle():
     import oracle as O  # test infrastructure only
     O.lib()
     return O
+
+
+# The GPU tests compare the gfx950 kernels with the oracle, so host-buffer
+# calls must reach the GPU whatever their size: switch the CPU/GPU crossover
+# off for this process (read once, when the library first codes).  The
+# crossover itself is tested in a child process with the defaults
+# (tests/test_gpu_engine.py).
+os.environ.setdefault("EC_CPU_BELOW_KB", "0")
+os.environ.setdefault("EC_GPU_INFLIGHT_MB", "1000000")
