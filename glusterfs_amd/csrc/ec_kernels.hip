@@ -85,8 +85,10 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-/* NW: waves per block for a single pattern; NWM: for mixed patterns */
-template <int K, int TS, int NW, int NWM, bool NTS>
+/* NW: waves per block for a single pattern; NWM: for mixed patterns;
+ * JTS / JTM: multiply through the jump table (ec_gf8_asm.h) instead of the
+ * compiler's switch, for single / mixed patterns */
+template <int K, int TS, int NW, int NWM, bool NTS, bool JTS, bool JTM>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     const uint64_t g = combine_grid<TS>(a.nstripes);
@@ -97,19 +99,19 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
     const size_t lds = combine_lds<TS>(a.k);
     if (a.patg) {
         /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
+        const void *kern = (const void *)ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM>;
         if (lds + kPatLdsBytes > (64u << 10) &&
-            ensure_lds_limit((const void *)ec_combine<K, TS, NWM, true, NTS, 2, true>,
-                             (int)(combine_lds<TS>(K) + kPatLdsBytes)) != 0)
+            ensure_lds_limit(kern, (int)(combine_lds<TS>(K) + kPatLdsBytes)) != 0)
             return -EIO;
-        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, true>), dim3((u32)g),
+        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM>), dim3((u32)g),
                            dim3(NWM * 64), lds + kPatLdsBytes, s, a);
     }
     else if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS>), dim3((u32)g), dim3(NWM * 64),
-                           lds, s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, false, true, JTM>), dim3((u32)g),
+                           dim3(NWM * 64), lds, s, a);
     else
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS>), dim3((u32)g), dim3(NW * 64), lds,
-                           s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS, 2, false, true, JTS>), dim3((u32)g),
+                           dim3(NW * 64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -262,8 +264,12 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
     if (a.group_pattern && a.group_shift < 3)
         return launch_combine_fine(s, a);
     /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
+    /* the jump-table multiply (r02, profiles/kbench_r02d.log): 16+4 decode
+     * 0.571 -> 0.680 of 8 TB/s (the compare tree's scalar work was the
+     * bound), 8+4 mixed 0.701 -> 0.717, 8+4 single pattern a tie, 4+2 a
+     * loss (0.741 -> 0.685), so 4+2 keeps the switch */
     if (a.k <= 4)
-        return launch_combine<4, 1, 8, 8, NTS>(s, a);
+        return launch_combine<4, 1, 8, 8, NTS, false, false>(s, a);
     if (a.k <= 8) {
         /* Full decodes (rows > 4) of up to 128K stripes use 16-wave blocks:
          * 64K-stripe batches (BASELINE configs[2]) 99.5 -> 91 us for 0xFF0,
@@ -272,10 +278,10 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
          * (profiles/kbench_r01_ts_*.log, ab_r01_nw16.log).  Heal-shaped
          * calls (rows <= 4) keep 4 waves. */
         if (a.rows > 4 && a.nstripes <= (1u << 17))
-            return launch_combine<8, 1, 16, 8, NTS>(s, a);
-        return launch_combine<8, 1, 4, 8, NTS>(s, a);
+            return launch_combine<8, 1, 16, 8, NTS, false, true>(s, a);
+        return launch_combine<8, 1, 4, 8, NTS, false, true>(s, a);
     }
-    return launch_combine<16, 1, 16, 16, NTS>(s, a);
+    return launch_combine<16, 1, 16, 16, NTS, true, true>(s, a);
 }
 
 /* pack, then launch; -E2BIG from the packer means "use a device table" */

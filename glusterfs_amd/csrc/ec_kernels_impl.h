@@ -408,29 +408,8 @@ __device__ __forceinline__ u32 tile_pattern(const CombineArgs &a, uint64_t t0)
  * one lane address serves all 8 planes of an input (ds_read2st64_b64 with
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
-/* LDS reads of one input's 8 planes: the compiler pairs them into
- * ds_read2st64_b64 (LDS table of MI355X_MICROARCH.md: 128 B/clk/CU); LDSR = 1
- * issues 8 single ds_read_b64 (256 B/clk/CU) and waits for them once. */
-template <int CW>
-__device__ __forceinline__ void lds_planes_b64(const uint8_t *src, u32 stride, u32 (&y)[8][CW])
-{
-    static_assert(CW == 2, "single-read form is written for 2 dwords per lane");
-    const u32 a = (u32)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)src;
-    uint2 v[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-        asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v[b]) : "v"(a), "i"(b * 512));
-    (void)stride;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        y[b][0] = v[b].x;
-        y[b][1] = v[b].y;
-    }
-}
-
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, int LDSR = 0>
+          bool CSE = true, bool JT = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -491,20 +470,22 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 #pragma unroll
             for (int w = 0; w < CW; ++w)
                 acc[b][w] = 0;
+        /* not unrolled: every copy of the loop body is a copy of the 255
+         * multiply programs (~54 KiB of code) */
+#pragma unroll 1
         for (u32 p = 0; p < k; ++p) {
             const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
             const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
             if (c == 0)                  /* ec-code-c.c:11666-11676 */
                 continue;
             const uint8_t *src = col + p * (T * ECD_CHUNK);
-            if constexpr (LDSR == 1 && T == 8 && CW == 2) {
-                lds_planes_b64<CW>(src, T * 64u, y);
-            } else {
 #pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
-            }
-            ecgf::mul_xor_rt<CW, CSE>(c, acc, y);
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+            if constexpr (JT && CW == 2)
+                ecgf::mul_xor_jt<CW>(c, acc, y);
+            else
+                ecgf::mul_xor_rt<CW, CSE>(c, acc, y);
         }
         const uint64_t ost = t0 + s;
         if (ost < a.nstripes)
@@ -571,6 +552,9 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
 #pragma unroll
         for (int b = 0; b < 8; ++b)
             acc[b][0] = acc[b][1] = 0;
+        /* not unrolled: every copy of the loop body is a copy of the 255
+         * multiply programs (~54 KiB of code) */
+#pragma unroll 1
         for (u32 p = 0; p < k; ++p) {
             const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
             const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);

@@ -319,9 +319,9 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     add("TS1 NW16 NTS", ec_combine<K, 1, 16, false, true>, 1, 16);
     add("TS1 NW16 NTS naive", ec_combine<K, 1, 16, false, true, 2, false, false>, 1, 16);
     add("TS1 NW16 NTS CW1", ec_combine<K, 1, 16, false, true, 1>, 1, 16);
-    add("TS1 NW8 NTS ldsb64", ec_combine<K, 1, 8, false, true, 2, false, true, 1>, 1, 8);
-    add("TS1 NW16 NTS ldsb64", ec_combine<K, 1, 16, false, true, 2, false, true, 1>, 1, 16);
-    add("TS1 NW4 NTS ldsb64", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 1, 4);
+    add("TS1 NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, true>, 1, 4);
+    add("TS1 NW8 NTS jt", ec_combine<K, 1, 8, false, true, 2, false, true, true>, 1, 8);
+    add("TS1 NW16 NTS jt", ec_combine<K, 1, 16, false, true, 2, false, true, true>, 1, 16);
     if constexpr (K <= 8) {   /* CW = 4: 16 stripes per item, 16-stripe tiles */
         add("TS2 NW8 NTS CW4", ec_combine<K, 2, 8, false, true, 4>, 2, 8);
         add("TS2 NW16 NTS CW4", ec_combine<K, 2, 16, false, true, 4>, 2, 16);
@@ -445,6 +445,7 @@ int main(int argc, char **argv)
         };
         addh("heal NW4 NTS", ec_combine<K, 1, 4, false, true>, 4);
         addh("heal NW4 NTS naive", ec_combine<K, 1, 4, false, true, 2, false, false>, 4);
+        addh("heal NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, true>, 4);
         addh("heal NW8 NTS", ec_combine<K, 1, 8, false, true>, 8);
         addh("heal NW16 NTS", ec_combine<K, 1, 16, false, true>, 16);
         run_group("heal 8+4 (regenerate 4 rows)", v, rounds, iters, s);
@@ -516,6 +517,8 @@ int main(int argc, char **argv)
         };
         addm("mixed TS1 NW4 NTS", ec_combine<K, 1, 4, true, true>, 4);
         addm("mixed TS1 NW8 NTS naive", ec_combine<K, 1, 8, true, true, 2, false, false>, 8);
+        addm("mixed TS1 NW8 NTS jt", ec_combine<K, 1, 8, true, true, 2, false, true, true>, 8);
+        addm("mixed TS1 NW4 NTS jt", ec_combine<K, 1, 4, true, true, 2, false, true, true>, 4);
         addm("mixed TS1 NW8 NTS", ec_combine<K, 1, 8, true, true>, 8);
         addm("mixed TS1 NW16 NTS", ec_combine<K, 1, 16, true, true>, 16);
         run_group("decode 8+4 mixed (16 patterns, 1024-stripe groups)", v, rounds, iters, s);
