@@ -17,12 +17,21 @@ The JSON line also carries
                 stream; `traffic` = PMC-measured HBM bytes per launch from the
                 committed rocprofv3 run (profiles/traffic.json)
   cpu_baseline  the CPU oracle (oracle/, C restatement of the reference
-                algorithm) decoding a bounded sample of the same fragments on
-                16 host threads, rank 0 at N=1 only
+                algorithm) on the host's usable cores and on one thread:
+                BASELINE configs[0] (4+2 encode of 1 GiB) and the bench
+                workload (4+2 decode), rank 0 at N=1 only
   extra         (N=1) the other BASELINE configs measured the same way, a
-                copy calibration, and PCIe-inclusive end-to-end rates
+                copy calibration, PCIe-inclusive end-to-end rates and the
+                library's own CPU engine
+
+Input data is the xorshift64 stream of SURVEY.md 8(d), generated on the
+GPU (glusterfs_amd/synth.py); rank r of an N-GPU job owns the r-th slice of
+one stream.  Full-size results are checked against the SHA-256 fixtures of
+tests/golden/fullsize_sha256.json (oracle-generated in the container):
+input, every encoded fragment, and decode outputs (= the input).
 """
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -61,11 +70,31 @@ def gbps(nbytes, seconds):
 
 
 def rand_u8(torch, nbytes, seed, device):
+    """Random bytes for the configs without a fixture (partial writes)."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     x = torch.randint(-2**62, 2**62, (nbytes // 8,), dtype=torch.int64, device=device,
                       generator=g)
     return x.view(torch.uint8)
+
+
+_FIX = None
+
+
+def fixture(case, rank):
+    """Full-size SHA-256 fixture of `case` for `rank`, or None."""
+    global _FIX
+    if _FIX is None:
+        try:
+            with open(os.path.join(ROOT, "tests", "golden", "fullsize_sha256.json")) as f:
+                _FIX = json.load(f)["cases"]
+        except (OSError, ValueError, KeyError):
+            _FIX = {}
+    return _FIX.get("%s_r%d" % (case, rank))
+
+
+def sha_dev(t):
+    return hashlib.sha256(memoryview(t.cpu().numpy())).hexdigest()
 
 
 def timed(torch, fn, steps, warmup, group=None):
@@ -91,53 +120,71 @@ def timed(torch, fn, steps, warmup, group=None):
 
 
 class Ctx:
-    def __init__(self, g, torch, dev):
-        self.g, self.torch, self.dev = g, torch, dev
+    def __init__(self, g, torch, dev, rank=0):
+        self.g, self.torch, self.dev, self.rank = g, torch, dev, rank
         self.sp = torch.cuda.current_stream(dev).cuda_stream
+        self.checks = {}
 
-    def encoded(self, k, n, nbytes, seed):
+    def encoded(self, k, n, nbytes, case=None):
+        """This rank's slice of the xorshift stream, encoded on the GPU; with
+        a fixture, the input and every fragment are checked by SHA-256."""
+        from glusterfs_amd import synth
         torch = self.torch
         nst = nbytes // (CHUNK * k)
-        data = rand_u8(torch, nst * CHUNK * k, seed, self.dev)
+        user = nst * CHUNK * k
+        data = synth.fill_device(torch, user, self.dev, word0=self.rank * user // 8)
         frags = [torch.empty(nst * CHUNK, dtype=torch.uint8, device=self.dev) for _ in range(n)]
         L = self.g.ECMatrixList(k, n)
         L.encode_device(self.dev.index, self.sp, nst, data, frags)
+        fx = fixture(case, self.rank) if case else None
+        if fx and fx["bytes"] == user and fx["k"] == k:
+            torch.cuda.synchronize()
+            ok = sha_dev(data) == fx["data"]
+            if "frags" in fx:
+                ok = ok and all(sha_dev(f) == h for f, h in zip(frags, fx["frags"]))
+            self.checks["%s_r%d" % (case, self.rank)] = ok
         return L, data, frags, nst
 
 
-def run_decode(c, k, n, nbytes, mask, steps, warmup, seed, group=None):
-    L, data, frags, nst = c.encoded(k, n, nbytes, seed)
+def run_decode(c, k, n, nbytes, mask, steps, warmup, case=None, group=None):
+    L, data, frags, nst = c.encoded(k, n, nbytes, case)
     rows = c.g.mask_rows(mask)
     ins = [frags[r - 1] for r in rows]
     out = c.torch.empty_like(data)
     wall, kt = timed(c.torch, lambda: L.decode_device(c.dev.index, c.sp, nst, mask, ins, out),
                      steps, warmup, group)
-    ok = bool(c.torch.equal(out, data))
+    ok = bool(c.torch.equal(out, data)) and c.checks.get("%s_r%d" % (case, c.rank), True)
     return dict(wall=wall, kernel_s=kt, ok=ok, user=nst * CHUNK * k, nst=nst, frags=frags,
                 rows=rows)
 
 
-def run_encode(c, k, n, nbytes, steps, warmup, seed, group=None):
+def run_encode(c, k, n, nbytes, steps, warmup, case=None, group=None):
     torch = c.torch
-    L, data, frags, nst = c.encoded(k, n, nbytes, seed)
+    L, data, frags, nst = c.encoded(k, n, nbytes, case)
     wall, kt = timed(torch, lambda: L.encode_device(c.dev.index, c.sp, nst, data, frags),
                      steps, warmup, group)
-    rows = list(range(n - k + 1, n + 1))
-    out = torch.empty_like(data)
-    L.decode_device(c.dev.index, c.sp, nst, sum(1 << (r - 1) for r in rows),
-                    [frags[r - 1] for r in rows], out)
-    torch.cuda.synchronize()
-    return dict(wall=wall, kernel_s=kt, ok=bool(torch.equal(out, data)), user=nst * CHUNK * k)
+    fx = fixture(case, c.rank) if case else None
+    if fx and "frags" in fx and fx["bytes"] == nst * CHUNK * k:
+        torch.cuda.synchronize()        # the timed launches rewrote the fragments
+        ok = all(sha_dev(f) == h for f, h in zip(frags, fx["frags"]))
+    else:
+        rows = list(range(n - k + 1, n + 1))
+        out = torch.empty_like(data)
+        L.decode_device(c.dev.index, c.sp, nst, sum(1 << (r - 1) for r in rows),
+                        [frags[r - 1] for r in rows], out)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(out, data))
+    return dict(wall=wall, kernel_s=kt, ok=ok, user=nst * CHUNK * k)
 
 
-def run_mixed(c, k, n, nbytes, steps, warmup, seed, group_stripes=1024, nmasks=16,
-              group=None):
+def run_mixed(c, k, n, nbytes, steps, warmup, case=None, group_stripes=1024, nmasks=16,
+              group=None, seed=17):
     """Self-heal reconstruct (configs[4]): every 1024-stripe group is decoded
     from its own k-of-n brick set, drawn (seeded) from `nmasks` masks."""
     import random
     torch = c.torch
-    L, data, frags, nst = c.encoded(k, n, nbytes, seed)
-    rnd = random.Random(seed)
+    L, data, frags, nst = c.encoded(k, n, nbytes, case)
+    rnd = random.Random(seed + 101 * c.rank)
     nmasks = min(nmasks, math.comb(n, k))
     masks = []
     while len(masks) < nmasks:
@@ -151,14 +198,15 @@ def run_mixed(c, k, n, nbytes, steps, warmup, seed, group_stripes=1024, nmasks=1
     wall, kt = timed(torch, lambda: L.decode_mixed_device(c.dev.index, c.sp, nst, group_stripes,
                                                           gp, masks, frags, out), steps, warmup,
                      group)
-    return dict(wall=wall, kernel_s=kt, ok=bool(torch.equal(out, data)), user=nst * CHUNK * k)
+    ok = bool(torch.equal(out, data)) and c.checks.get("%s_r%d" % (case, c.rank), True)
+    return dict(wall=wall, kernel_s=kt, ok=ok, user=nst * CHUNK * k)
 
 
-def run_heal(c, k, n, nbytes, steps, warmup, seed):
+def run_heal(c, k, n, nbytes, steps, warmup, case=None):
     """Fused heal: regenerate the r lost fragments
     directly from k good ones (reads S, writes r*S/k)."""
     torch = c.torch
-    L, data, frags, nst = c.encoded(k, n, nbytes, seed)
+    L, data, frags, nst = c.encoded(k, n, nbytes, case)
     good = list(range(n - k, n))                 # bricks 0..r-1 lost
     mask = sum(1 << b for b in good)
     target = ((1 << n) - 1) & ~mask
@@ -222,7 +270,8 @@ def run_e2e(c, k, n, nbytes, steps, group=None):
     try:
         din_p, din = pinned(S)
         bufs.append(din_p)
-        din[:] = rand_u8(c.torch, S, 99, c.dev).cpu().numpy()
+        from glusterfs_amd import synth
+        din[:] = synth.fill_numpy(S)
         fr = [pinned(nst * CHUNK) for _ in range(n)]
         bufs += [p for p, _ in fr]
         dout_p, dout = pinned(S)
@@ -276,30 +325,30 @@ def extra_configs(c, steps, warmup):
         ex[name] = dict(user_GBps=round(gbps(r["user"], r["kernel_s"]), 1),
                         hbm_frac=frac(alg, r["kernel_s"]), ok=r["ok"])
 
-    r = run_encode(c, 4, 6, 1 << 30, st, warmup, 11)
+    r = run_encode(c, 4, 6, 1 << 30, st, warmup, "4+2_1GiB")
     put("enc_4+2_1GiB", r, 2.5 * r["user"])
-    r = run_decode(c, 4, 6, 1 << 30, 0x0F, st, warmup, 14)
+    r = run_decode(c, 4, 6, 1 << 30, 0x0F, st, warmup, "4+2_1GiB")
     put("dec_4+2_0x0F_1GiB", r, 2 * r["user"])
     nb = 65536 * CHUNK * 8                       # configs[2]: 64K-stripe batches
-    r = run_encode(c, 8, 12, nb, st, warmup, 12)
+    r = run_encode(c, 8, 12, nb, st, warmup, "8+4_64Kstripes")
     put("enc_8+4_64Kstripes", r, 2.5 * r["user"])
     for name, mask in (("dec_8+4_0xFF0_64Kstripes", 0xFF0),
                        ("dec_8+4_0xEB5_64Kstripes", 0xEB5)):
-        r = run_decode(c, 8, 12, nb, mask, st, warmup, 13)
+        r = run_decode(c, 8, 12, nb, mask, st, warmup, "8+4_64Kstripes")
         put(name, r, 2 * r["user"])
-    r = run_decode(c, 8, 12, 1 << 30, 0xFF0, st, warmup, 16)
+    r = run_decode(c, 8, 12, 1 << 30, 0xFF0, st, warmup, "8+4_1GiB")
     put("dec_8+4_0xFF0_1GiB", r, 2 * r["user"])
-    r = run_encode(c, 16, 20, 2 << 30, st, warmup, 15)
+    r = run_encode(c, 16, 20, 2 << 30, st, warmup, "16+4_2GiB")
     put("enc_16+4_2GiB", r, 2.25 * r["user"])
-    r = run_decode(c, 16, 20, 1 << 30, 0xFFFF0, st, warmup, 20)
+    r = run_decode(c, 16, 20, 1 << 30, 0xFFFF0, st, warmup, "16+4_1GiB")
     put("dec_16+4_0xFFFF0_1GiB", r, 2 * r["user"])
-    r = run_mixed(c, 8, 12, 1 << 30, st, warmup, 17)
+    r = run_mixed(c, 8, 12, 1 << 30, st, warmup, "8+4_1GiB")
     put("selfheal_mixed16_8+4_1GiB", r, 2 * r["user"])
     # 64 masks of a 16+4 volume: past the kernel-argument space (7 matrices),
     # the decode matrices come from the per-call device table
-    r = run_mixed(c, 16, 20, 1 << 30, st, warmup, 21, nmasks=64)
+    r = run_mixed(c, 16, 20, 1 << 30, st, warmup, "16+4_1GiB", nmasks=64, seed=21)
     put("selfheal_mixed64_16+4_1GiB", r, 2 * r["user"])
-    r = run_heal(c, 8, 12, 1 << 30, st, warmup, 18)
+    r = run_heal(c, 8, 12, 1 << 30, st, warmup, "8+4_1GiB")
     put("heal_fused_8+4_regen4_1GiB", r, r["alg"])
     r = run_writev(c, 4, 6, (1 << 30) + 777, st, warmup, 19)
     put("writev_rmw_4+2_1GiB_unaligned", r, r["alg"])
@@ -309,6 +358,7 @@ def extra_configs(c, steps, warmup):
             ex[name] = run_e2e(c, k, n, 512 << 20, 3)
         except Exception as exc:                 # reported, never fatal to the bench line
             ex[name] = dict(error=repr(exc)[:200])
+    ex["fullsize_sha256_checks"] = dict(c.checks)
     return ex
 
 
@@ -331,11 +381,11 @@ def dist_configs(c, grp, steps, warmup):
                         ok=ok)
 
     # configs[3]: 16+4 encode, stripe-range partitioned (2 GiB per GPU)
-    r = run_encode(c, 16, 20, 2 << 30, st, warmup, 15 + 101 * grp.rank, grp)
+    r = run_encode(c, 16, 20, 2 << 30, st, warmup, "16+4_2GiB", group=grp)
     put("dist_enc_16+4_2GiB_per_gpu", r, 2.25)
     del r
     # configs[4]: self-heal reconstruct, mixed patterns (1 GiB per GPU)
-    r = run_mixed(c, 8, 12, 1 << 30, st, warmup, 17 + 101 * grp.rank, group=grp)
+    r = run_mixed(c, 8, 12, 1 << 30, st, warmup, "8+4_1GiB", group=grp)
     put("dist_selfheal_mixed16_8+4_1GiB_per_gpu", r, 2.0)
     del r
     torch.cuda.empty_cache()
@@ -349,43 +399,133 @@ def dist_configs(c, grp, steps, warmup):
             buffers="pinned host, one GPU per rank (EC_MI355X_HOST_DEVICES)")
     except Exception as exc:                     # reported, never fatal to the bench line
         ex["dist_e2e_pcie_16+4_512MiB_per_gpu"] = dict(error=repr(exc)[:200])
+    ex["fullsize_sha256_checks_all_ranks"] = grp.all_ok(all(c.checks.values()))
     return ex
 
 
-def cpu_baseline(sample_frags, rows, k, n, budget_s=10.0):
-    """The oracle's C restatement (ec_code_c_interleaved / _linear with
-    straight-line per-constant muladds, oracle/gen_muladd.py) on `threads`
-    host threads over a bounded sample of the same fragments: decode (the
-    bench workload, `value`) for ~budget_s, then encode of the decoded
-    sample for ~budget_s/2.  Output buffers are reused across passes, as
-    the reference reuses its iobufs."""
+def host_cpus():
+    """What the host offers this process: nproc, the CPUs it may run on, the
+    cgroup CPU quota, the model -- and the thread count to use (the smaller
+    of affinity and quota)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    threads = min(aff, quota) if quota else aff
+    return dict(nproc=nproc, affinity=aff, cgroup_quota=quota, model=model, threads=threads)
+
+
+def _rate(fn, nbytes, budget):
+    fn()                                   # warm: faults the outputs in
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        fn()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget or passes >= 10000:
+            return round(nbytes * passes / el / 1e9, 3), passes
+
+
+def cpu_baseline(budget_s=4.0):
+    """The oracle's C restatement (oracle/ec_oracle.c: ec_code_c_linear /
+    _interleaved with straight-line per-constant muladds, the speed class of
+    the reference's portable C path) on the host's usable cores and on one
+    thread.  BASELINE configs[0]: 4+2 encode of 1 GiB of the xorshift stream;
+    and the bench workload, 4+2 decode of the same 1 GiB with bricks 0, 1
+    lost.  Output buffers are reused across passes, as the reference reuses
+    its iobufs.  The encode output is checked against the fixture."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # test infrastructure: the CPU baseline leg only
-    threads = min(16, os.cpu_count() or 1)
-    user = sample_frags[0].size * k
+    hc = host_cpus()
+    T = hc["threads"]
+    k, n, S = 4, 6, 1 << 30
+    data = O.fill_xorshift(S)
+    frags = [np.empty(S // k, dtype=np.uint8) for _ in range(n)]
+    rows = [3, 4, 5, 6]
+    out = np.empty(S, dtype=np.uint8)
+    enc_T, enc_p = _rate(lambda: O.encode(k, n, data, nthreads=T, out=frags), S, budget_s)
+    fx = fixture("4+2_1GiB", 0)
+    enc_ok = bool(fx) and all(hashlib.sha256(memoryview(f)).hexdigest() == h
+                              for f, h in zip(frags, fx["frags"]))
+    ins = [frags[r - 1] for r in rows]
+    dec_T, dec_p = _rate(lambda: O.decode(k, rows, ins, nthreads=T, out=out), S, budget_s)
+    enc_1, _ = _rate(lambda: O.encode(k, n, data, nthreads=1, out=frags), S, 0.5)
+    dec_1, _ = _rate(lambda: O.decode(k, rows, ins, nthreads=1, out=out), S, 0.5)
+    return dict(value=dec_T, unit="GB/s", cores=T, kind="port", threads=T,
+                nproc=hc["nproc"], affinity_cpus=hc["affinity"],
+                cgroup_cpu_quota=hc["cgroup_quota"], model=hc["model"],
+                encode_1GiB_GBps=enc_T, one_thread_encode_GBps=enc_1,
+                one_thread_decode_GBps=dec_1, encode_matches_fixture=enc_ok,
+                sample="oracle/ec_oracle.c (portable-C class restatement; the reference's "
+                       "default engine is the AVX JIT, BASELINE.md) on %d threads: 4+2 decode "
+                       "of 1 GiB, mask 0x3C, %d passes (value); configs[0] 4+2 encode of 1 GiB "
+                       "xorshift input, %d passes (encode_1GiB_GBps); one-thread figures over "
+                       ">= 0.5 s" % (T, dec_p, enc_p))
 
-    def timed(fn, budget):
-        fn()                                   # warm: faults the outputs in
-        t0 = time.perf_counter()
-        passes = 0
-        while True:
-            fn()
-            passes += 1
-            el = time.perf_counter() - t0
-            if el >= budget or passes >= 100000:
-                return passes, el
 
-    out = np.empty(user, dtype=np.uint8)
-    dp, de = timed(lambda: O.decode(k, rows, sample_frags, nthreads=threads, out=out), budget_s)
-    frags = [np.empty(user // k, dtype=np.uint8) for _ in range(n)]
-    ep, ee = timed(lambda: O.encode(k, n, out, nthreads=threads, out=frags), budget_s / 2)
-    return dict(value=round(user * dp / de / 1e9, 3), unit="GB/s", cores=threads,
-                kind="port", encode_GBps=round(user * ep / ee / 1e9, 3),
-                sample="oracle/ec_oracle.c %d+%d decode (ec_code_c_interleaved restatement), "
-                       "mask 0x3C, %d MiB of user data x %d passes, %d threads; encode of the "
-                       "same %d MiB x %d passes (encode_GBps)" %
-                       (k, n - k, user >> 20, dp, threads, user >> 20, ep))
+def cpu_engine_rates(threads, budget_s=2.0):
+    """The library's own CPU engine (ec_cpu*.c; cpu-extensions=avx) on host
+    buffers: 4+2 encode and decode of 1 GiB on one thread, and on `threads`
+    threads each coding its own 1/threads of it (how concurrent GlusterFS
+    fops use it: one call per calling thread)."""
+    import threading
+    import numpy as np
+    import glusterfs_amd as g
+    from glusterfs_amd import synth
+    k, n, S = 4, 6, 1 << 30
+    nst = S // (CHUNK * k)
+    data = synth.fill_numpy(S)
+    frags = [np.empty(S // k, np.uint8) for _ in range(n)]
+    out = np.empty(S, np.uint8)
+    rows = [3, 4, 5, 6]
+    res = {}
+    with g.ECMatrixList(k, n, gen="avx") as L:
+        res["engine"] = L.engine
+
+        def enc(t0, t1):
+            L.encode_batch(t1 - t0, data[t0 * CHUNK * k:],
+                           [f[t0 * CHUNK:] for f in frags])
+
+        def dec(t0, t1):
+            L.decode_batch(t1 - t0, 0x3C, rows, [frags[r - 1][t0 * CHUNK:] for r in rows],
+                           out[t0 * CHUNK * k:])
+
+        def par(fn):
+            def run():
+                th = [threading.Thread(target=fn, args=(nst * i // threads,
+                                                         nst * (i + 1) // threads))
+                      for i in range(threads)]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join()
+            return run
+
+        res["one_thread_encode_GBps"], _ = _rate(lambda: enc(0, nst), S, budget_s / 2)
+        res["one_thread_decode_GBps"], _ = _rate(lambda: dec(0, nst), S, budget_s / 2)
+        res["threads"] = threads
+        res["encode_GBps"], _ = _rate(par(enc), S, budget_s)
+        res["decode_GBps"], _ = _rate(par(dec), S, budget_s)
+        res["ok"] = bool(np.array_equal(out, data))
+    return res
 
 
 def only(c, spec, nbytes, steps, warmup):
@@ -393,17 +533,17 @@ def only(c, spec, nbytes, steps, warmup):
     k, r = map(int, parts[1].split("+"))
     n = k + r
     if parts[0] == "enc":
-        res = run_encode(c, k, n, nbytes, steps, warmup, 1)
+        res = run_encode(c, k, n, nbytes, steps, warmup)
     elif parts[0] == "dec":
-        res = run_decode(c, k, n, nbytes, int(parts[2], 16), steps, warmup, 1)
+        res = run_decode(c, k, n, nbytes, int(parts[2], 16), steps, warmup)
     elif parts[0] == "mixed":
         nm = int(parts[2]) if len(parts) > 2 else 16
         gs = int(parts[3]) if len(parts) > 3 else 1024
-        res = run_mixed(c, k, n, nbytes, steps, warmup, 1, group_stripes=gs, nmasks=nm)
+        res = run_mixed(c, k, n, nbytes, steps, warmup, group_stripes=gs, nmasks=nm)
     elif parts[0] == "rmw":
         res = run_writev(c, k, n, nbytes + 777, steps, warmup, 1)
     else:
-        res = run_heal(c, k, n, nbytes, steps, warmup, 1)
+        res = run_heal(c, k, n, nbytes, steps, warmup)
     print(json.dumps(dict(only=spec, kernel_ms=res["kernel_s"] * 1e3, ok=res["ok"])))
 
 
@@ -448,13 +588,13 @@ def main():
     torch.cuda.set_device(dev_index)          # before the process group (NCCL)
     grp = Group()
     dev = torch.device("cuda", dev_index)
-    c = Ctx(g, torch, dev)
+    c = Ctx(g, torch, dev, grp.rank)
     nbytes = int(args.gib * (1 << 30))
     if args.only:
         return only(c, args.only, nbytes, args.steps, args.warmup)
 
     k, n, mask = 4, 6, 0x3C
-    r = run_decode(c, k, n, nbytes, mask, args.steps, args.warmup, 1234 + grp.rank, grp)
+    r = run_decode(c, k, n, nbytes, mask, args.steps, args.warmup, "4+2_1GiB", grp)
     wall = grp.max(r["wall"])
     ok = grp.all_ok(r["ok"])
     value = gbps(r["user"] * grp.world * args.steps, wall)
@@ -482,7 +622,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (torch.randint bytes, fixed seed per rank), encoded on-GPU",
+        "data": "synthetic: xorshift64 stream of SURVEY 8(d), rank r = r-th slice, generated "
+                "and encoded on-GPU; input, fragments and output checked against the "
+                "oracle's full-size SHA-256 fixtures",
         "config": {
             "workload": "disperse 4+2 decode, 2 fragments missing (mask 0x3C), "
                         "%d MiB user data per GPU per step (BASELINE configs[1])" %
@@ -504,10 +646,7 @@ def main():
             "avg_launch_ms": round(kt * 1e3, 4),
         },
     }
-    frags_host = None
-    if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
-        fs = (128 << 20) // k                  # 128 MiB of user data
-        frags_host = [r["frags"][x - 1][:fs].cpu().numpy() for x in r["rows"]]
+    out["fullsize_sha256_check"] = c.checks.get("4+2_1GiB_r%d" % grp.rank)
     del r
     torch.cuda.empty_cache()
     extra = args.extra if args.extra is not None else grp.world == 1
@@ -515,8 +654,14 @@ def main():
         out["extra"] = extra_configs(c, args.steps, args.warmup)
     elif grp.world > 1 and not args.no_dist_extra:
         out["extra"] = dist_configs(c, grp, args.steps, args.warmup)
-    if frags_host is not None:
-        out["cpu_baseline"] = cpu_baseline(frags_host, [3, 4, 5, 6], k, n)
+    if grp.rank == 0 and grp.world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline()
+        if extra:
+            try:
+                out["extra"]["cpu_engine_4+2_1GiB"] = cpu_engine_rates(
+                    out["cpu_baseline"]["threads"])
+            except Exception as exc:             # reported, never fatal to the bench line
+                out["extra"]["cpu_engine_4+2_1GiB"] = dict(error=repr(exc)[:200])
     grp.barrier()
     if grp.rank == 0:
         print(json.dumps(out))

@@ -30,6 +30,7 @@
 
 #include <errno.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -258,9 +259,21 @@ int launch_combine_fine(hipStream_t s, const CombineArgs &a)
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+/* EC_MI355X_JT=0 / 1 forces the switch / the jump table for every k
+ * (tuning A/Bs on one box, tools/ab_jt.sh); unset = the shipped choice. */
+int jt_override()
+{
+    static const int v = [] {
+        const char *e = getenv("EC_MI355X_JT");
+        return e && (*e == '0' || *e == '1') ? *e - '0' : -1;
+    }();
+    return v;
+}
+
 template <bool NTS>
 int launch_combine_k(hipStream_t s, const CombineArgs &a)
 {
+    const int jt = jt_override();
     if (a.group_pattern && a.group_shift < 3)
         return launch_combine_fine(s, a);
     /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
@@ -269,8 +282,16 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
      * bound), 8+4 mixed 0.701 -> 0.717, 8+4 single pattern a tie, 4+2 a
      * loss (0.741 -> 0.685), so 4+2 keeps the switch */
     if (a.k <= 4)
-        return launch_combine<4, 1, 8, 8, NTS, false, false>(s, a);
+        return jt == 1 ? launch_combine<4, 1, 8, 8, NTS, true, true>(s, a)
+                       : launch_combine<4, 1, 8, 8, NTS, false, false>(s, a);
     if (a.k <= 8) {
+        if (jt >= 0) {
+            if (a.rows > 4 && a.nstripes <= (1u << 17))
+                return jt ? launch_combine<8, 1, 16, 8, NTS, true, true>(s, a)
+                          : launch_combine<8, 1, 16, 8, NTS, false, false>(s, a);
+            return jt ? launch_combine<8, 1, 4, 8, NTS, true, true>(s, a)
+                      : launch_combine<8, 1, 4, 8, NTS, false, false>(s, a);
+        }
         /* Full decodes (rows > 4) of up to 128K stripes use 16-wave blocks:
          * 64K-stripe batches (BASELINE configs[2]) 99.5 -> 91 us for 0xFF0,
          * 108 -> 100 us for 0xEB5, same box, alternating libraries; at 1 GiB
@@ -281,7 +302,8 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
             return launch_combine<8, 1, 16, 8, NTS, false, true>(s, a);
         return launch_combine<8, 1, 4, 8, NTS, false, true>(s, a);
     }
-    return launch_combine<16, 1, 16, 16, NTS, true, true>(s, a);
+    return jt == 0 ? launch_combine<16, 1, 16, 16, NTS, false, false>(s, a)
+                   : launch_combine<16, 1, 16, 16, NTS, true, true>(s, a);
 }
 
 /* pack, then launch; -E2BIG from the packer means "use a device table" */
