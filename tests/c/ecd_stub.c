@@ -1,0 +1,38 @@
+/* Device layer stand-in for the host-only sanitizer build
+ * (tests/test_sanitizers.py): no GPU, so ec_method.c takes its CPU engine
+ * paths.  Every entry point of glusterfs_amd/csrc/ec_device.h. */
+#include <errno.h>
+#include <stddef.h>
+
+#include "../../glusterfs_amd/csrc/ec_device.h"
+
+int ecd_device_count(void) { return 0; }
+const char *ecd_last_error(void) { return "no device (sanitizer build)"; }
+int ecd_has_vander(uint32_t k, uint32_t n) { (void)k; (void)n; return 0; }
+int ecd_encode_vander(int d, void *s, uint32_t k, uint32_t n, uint64_t ns, const void *in,
+                      void *const *out)
+{ (void)d; (void)s; (void)k; (void)n; (void)ns; (void)in; (void)out; return -ENODEV; }
+int ecd_combine(int d, void *s, const ecd_combine_desc_t *x) { (void)d; (void)s; (void)x; return -ENODEV; }
+int ecd_sync(int d, void *s) { (void)d; (void)s; return -ENODEV; }
+int ecd_encode_host(int nd, uint32_t k, uint32_t n, uint64_t ns, const void *in, void *const *out,
+                    const uint8_t *p)
+{ (void)nd; (void)k; (void)n; (void)ns; (void)in; (void)out; (void)p; return -ENODEV; }
+int ecd_encode_host_gather(int nd, uint32_t k, uint32_t n, uint64_t ns, uint32_t sg,
+                           const void *const *sp, const uint64_t *sl, void *const *out,
+                           const uint8_t *p)
+{ (void)nd; (void)k; (void)n; (void)ns; (void)sg; (void)sp; (void)sl; (void)out; (void)p; return -ENODEV; }
+int ecd_writev_encode_device(int d, void *s, uint32_t k, uint32_t n, uint64_t h, uint64_t us,
+                             const void *u, const void *oh, const void *ot, void *const *out,
+                             const uint8_t *p)
+{ (void)d; (void)s; (void)k; (void)n; (void)h; (void)us; (void)u; (void)oh; (void)ot; (void)out; (void)p; return -ENODEV; }
+int ecd_decode_host(int nd, uint32_t k, uint32_t rows, uint64_t ns, uint32_t nf,
+                    const void *const *f, void *out, void *const *outs, uint32_t np,
+                    const uint8_t *p, const uint8_t *gp, uint32_t gs)
+{ (void)nd; (void)k; (void)rows; (void)ns; (void)nf; (void)f; (void)out; (void)outs; (void)np; (void)p; (void)gp; (void)gs; return -ENODEV; }
+int ecd_ptr_device(const void *p) { (void)p; return -1; }
+void *ecd_host_alloc(size_t b) { (void)b; return NULL; }
+void ecd_host_free(void *p) { (void)p; }
+int ecd_host_register(void *p, size_t b) { (void)p; (void)b; return -ENODEV; }
+int ecd_host_unregister(void *p) { (void)p; return -ENODEV; }
+int ecd_host_busy(uint64_t l) { (void)l; return 1; }
+void ecd_inject_faults(uint32_t n) { (void)n; }

@@ -1,0 +1,53 @@
+"""SURVEY.md 5 (race detection / sanitizers; reference: configure --enable-asan
+/ --enable-tsan, configure.ac:283-310): the host-only part of the library --
+ec_method.c (GF(2^8), matrices, the LRU cache of inverses, the on-disk config
+guard) and the CPU engine -- built with ASan+UBSan and with TSan around a
+device-layer stub, then driven by 8 threads sharing one list with a 3-entry
+cache (tests/c/sanitize_check.c).  CPU only; each build takes seconds."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "glusterfs_amd", "csrc")
+
+
+def build(tmp_path, san):
+    cc = shutil.which("gcc")
+    if cc is None:
+        pytest.skip("gcc not installed")
+    objs = []
+    common = ["-g", "-O1", "-fno-omit-frame-pointer", "-fPIC", "-std=gnu11", "-pthread",
+              "-I" + os.path.join(ROOT, "include"), "-I" + CSRC] + san
+    srcs = [(os.path.join(CSRC, "ec_method.c"), []), (os.path.join(CSRC, "ec_cpu.c"), []),
+            (os.path.join(ROOT, "tests", "c", "ecd_stub.c"), [])]
+    kerns = [("base", []), ("avx2", ["-mavx2"]), ("avx512", ["-mavx512f"])]
+    for i, (src, extra) in enumerate(srcs):
+        o = str(tmp_path / ("s%d.o" % i))
+        subprocess.run([cc, *common, *extra, "-c", src, "-o", o], check=True)
+        objs.append(o)
+    procs = []                          # the three kernel builds run in parallel
+    for sfx, flags in kerns:
+        o = str(tmp_path / ("k_%s.o" % sfx))
+        procs.append(subprocess.Popen([cc, *common, "-Wno-psabi",
+                                       "-fno-tree-loop-distribute-patterns", "-DECC_SFX=" + sfx,
+                                       *flags, "-c", os.path.join(CSRC, "ec_cpu_kern.c"),
+                                       "-o", o]))
+        objs.append(o)
+    assert all(p.wait() == 0 for p in procs)
+    exe = str(tmp_path / "sanitize_check")
+    subprocess.run([cc, *common, os.path.join(ROOT, "tests", "c", "sanitize_check.c"), *objs,
+                    "-o", exe], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("san", [["-fsanitize=address,undefined", "-fno-sanitize-recover=all"],
+                                 ["-fsanitize=thread"]], ids=["asan-ubsan", "tsan"])
+def test_host_layer_under_sanitizers(tmp_path, san):
+    exe = build(tmp_path, san)
+    env = dict(os.environ, EC_MI355X_QUIET="1", ASAN_OPTIONS="detect_leaks=1",
+               TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0 and "failures=0" in r.stdout, (r.stdout + r.stderr)[-4000:]
