@@ -89,10 +89,11 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
 /* NW: waves per block for a single pattern; NWM: for mixed patterns;
  * JTS / JTM: multiply through the jump table (ec_gf8_asm.h) instead of the
  * compiler's switch, for single / mixed patterns */
-template <int K, int TS, int NW, int NWM, bool NTS, bool JTS, bool JTM>
+template <int K, int TS, int NW, int NWM, bool NTS, bool JTS, bool JTM, bool SL = false>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
-    const uint64_t g = combine_grid<TS>(a.nstripes);
+    /* sorted slots: every pattern's run may carry up to 7 padding slots */
+    const uint64_t g = SL ? (a.nstripes + 8ull * a.npatterns) / 8 + 1 : combine_grid<TS>(a.nstripes);
     if (g == 0)
         return 0;
     if (g > 0x7fffffffull)
@@ -100,16 +101,16 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
     const size_t lds = combine_lds<TS>(a.k);
     if (a.patg) {
         /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
-        const void *kern = (const void *)ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM>;
+        const void *kern = (const void *)ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM, SL>;
         if (lds + kPatLdsBytes > (64u << 10) &&
             ensure_lds_limit(kern, (int)(combine_lds<TS>(K) + kPatLdsBytes)) != 0)
             return -EIO;
-        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM>), dim3((u32)g),
-                           dim3(NWM * 64), lds + kPatLdsBytes, s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM, SL>),
+                           dim3((u32)g), dim3(NWM * 64), lds + kPatLdsBytes, s, a);
     }
     else if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, false, true, JTM>), dim3((u32)g),
-                           dim3(NWM * 64), lds, s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, false, true, JTM, SL>),
+                           dim3((u32)g), dim3(NWM * 64), lds, s, a);
     else
         hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS, 2, false, true, JTS>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
@@ -244,19 +245,49 @@ int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-/* pattern groups of 1, 2 or 4 stripes: the per-stripe waterfall kernel */
-int launch_combine_fine(hipStream_t s, const CombineArgs &a)
+/* Pattern groups of 1, 2 or 4 stripes: sort the stripes by pattern into
+ * 8-slot tiles (ec_slots_*, ec_kernels_impl.h) and run the tile kernel over
+ * the slot list.  Workspace: stream-ordered, freed after the launch. */
+template <bool NTS>
+int launch_combine_slots(hipStream_t s, const CombineArgs &a0)
 {
-    const uint64_t g = (a.nstripes * 16 + 255) / 256;
-    if (g == 0)
+    if (a0.nstripes == 0)
         return 0;
-    if (g > 0x7fffffffull)
-        return -EINVAL;
-    if (a.patg)
-        hipLaunchKernelGGL(ec_combine_fine<true>, dim3((u32)g), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(ec_combine_fine<false>, dim3((u32)g), dim3(256), 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    if (a0.nstripes + 8ull * a0.npatterns >= 0xFFFFFFFFull)
+        return -EINVAL;                 /* slots hold 32-bit stripe numbers */
+    const uint64_t nslots_max = a0.nstripes + 8ull * a0.npatterns;
+    u32 *ws = nullptr;
+    const size_t bytes = (size_t)(512 + 1 + nslots_max) * 4;
+    if (hipMallocAsync(reinterpret_cast<void **>(&ws), bytes, s) != hipSuccess) {
+        (void)hipGetLastError();
+        return -ENOMEM;
+    }
+    u32 *counts = ws, *cursors = ws + 256, *total = ws + 512, *slots = ws + 513;
+    CombineArgs a = a0;
+    a.slot_stripe = slots;
+    a.slot_count = total;
+    const uint64_t nb = (a.nstripes + kSlotBlock * kSlotPerThread - 1) / (kSlotBlock * kSlotPerThread);
+    int rc = 0;
+    if (hipMemsetAsync(counts, 0, 256 * 4, s) != hipSuccess ||
+        hipMemsetAsync(slots, 0xFF, nslots_max * 4, s) != hipSuccess)
+        rc = -EIO;
+    if (rc == 0) {
+        hipLaunchKernelGGL(ec_slots_count, dim3((u32)nb), dim3(kSlotBlock), 0, s, a, counts);
+        hipLaunchKernelGGL(ec_slots_scan, dim3(1), dim3(256), 0, s, counts, cursors, total);
+        hipLaunchKernelGGL(ec_slots_scatter, dim3((u32)nb), dim3(kSlotBlock), 0, s, a, cursors,
+                           slots);
+        rc = hipGetLastError() == hipSuccess ? 0 : -EIO;
+    }
+    if (rc == 0) {
+        if (a.k <= 4)
+            rc = launch_combine<4, 1, 8, 8, NTS, false, false, true>(s, a);
+        else if (a.k <= 8)
+            rc = launch_combine<8, 1, 8, 8, NTS, false, true, true>(s, a);
+        else
+            rc = launch_combine<16, 1, 16, 16, NTS, true, true, true>(s, a);
+    }
+    (void)hipFreeAsync(ws, s);
+    return rc;
 }
 
 /* EC_MI355X_JT=0 / 1 forces the switch / the jump table for every k
@@ -275,7 +306,7 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
 {
     const int jt = jt_override();
     if (a.group_pattern && a.group_shift < 3)
-        return launch_combine_fine(s, a);
+        return launch_combine_slots<NTS>(s, a);
     /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
     /* the jump-table multiply (r02, profiles/kbench_r02d.log): 16+4 decode
      * 0.571 -> 0.680 of 8 TB/s (the compare tree's scalar work was the
@@ -331,7 +362,7 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
     if (d->k == 0 || d->k > ECD_MAX_K || d->rows == 0 || d->rows > ECD_MAX_ROWS)
         return -EINVAL;
     if (d->group_pattern && d->group_shift > 40)
-        return -EINVAL; /* groups below 8 stripes run ec_combine_fine */
+        return -EINVAL; /* groups below 8 stripes run through sorted slots */
     if (d->npatterns == 0 || d->npatterns > ECD_MAX_PATTERNS ||
         (!d->pat_ext && (uint64_t)d->npatterns * d->pat_bytes > ECD_MAX_PAT_BYTES) ||
         d->pat_bytes < d->k + d->rows * d->k)
@@ -343,6 +374,8 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
     a->nstripes = d->nstripes;
     a->group_pattern = d->group_pattern;
     a->patg = nullptr;
+    a->slot_stripe = nullptr;
+    a->slot_count = nullptr;
     a->k = d->k;
     a->kw = (d->k + 3) / 4;
     a->rows = d->rows;

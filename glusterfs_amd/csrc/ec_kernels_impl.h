@@ -321,6 +321,9 @@ struct CombineArgs {
     uint64_t in_stride, out_stride, nstripes;
     const uint8_t *group_pattern;
     const u32 *patg;        /* pattern table in device memory (PG kernels) */
+    /* sorted slots (SLOTS kernels): slot i holds stripe slot_stripe[i] or
+     * kNoStripe; every 8-slot tile is one pattern's; *slot_count slots */
+    const u32 *slot_stripe, *slot_count;
     u32 k, kw, rows, group_shift, pwords, npatterns;
     u32 pat[kPatWords];
 };
@@ -389,6 +392,9 @@ struct PatWords {
 
 constexpr size_t kPatLdsBytes = kMaxPatWords * 4; /* PG kernels: LDS after the tile */
 
+constexpr u32 kNoStripe = 0xFFFFFFFFu;        /* padding slot            */
+constexpr uint64_t kNoSlot = ~0ull;            /* "no stripe here" in tiles */
+
 /* pattern id of the tile starting at stripe t0 (ids past the table clamp to
  * the last pattern: a bad caller map must not fault the device) */
 template <bool MIXED>
@@ -400,6 +406,23 @@ __device__ __forceinline__ u32 tile_pattern(const CombineArgs &a, uint64_t t0)
     return id < a.npatterns ? id : a.npatterns - 1u;
 }
 
+/* Stripe of tile slot `slot`: the slot itself, or (SLOTS) the sorted list's
+ * entry -- kNoSlot past the data or in a run's padding. */
+template <bool SLOTS>
+__device__ __forceinline__ uint64_t slot_stripe(const CombineArgs &a, uint64_t slot,
+                                                u32 nslots)
+{
+    if constexpr (!SLOTS) {
+        (void)nslots;
+        return slot < a.nstripes ? slot : kNoSlot;
+    } else {
+        if (slot >= nslots)
+            return kNoSlot;
+        const u32 v = a.slot_stripe[slot];
+        return v == kNoStripe ? kNoSlot : (uint64_t)v;
+    }
+}
+
 /* K: max inputs (k <= K); TS: tile = 8*TS stripes; NW: waves per block.
  *
  * LDS tile, plane-major: input p, plane b, tile stripe s, 64-byte segment at
@@ -408,8 +431,11 @@ __device__ __forceinline__ u32 tile_pattern(const CombineArgs &a, uint64_t t0)
  * one lane address serves all 8 planes of an input (ds_read2st64_b64 with
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
+/* SLOTS: mixed patterns with groups below a tile (1, 2, 4 stripes): the
+ * stripes were sorted by pattern into 8-slot tiles (ec_slots_* kernels), and
+ * the block reads its tile's stripes from the slot list. */
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, bool JT = false>
+          bool CSE = true, bool JT = false, bool SLOTS = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -423,8 +449,16 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-
-    const PatWords<PG> pw(a, tile_pattern<MIXED>(a, t0), lane, lds + k * (T * ECD_CHUNK));
+    u32 nslots = 0;
+    if constexpr (SLOTS) {
+        nslots = __builtin_amdgcn_readfirstlane(*a.slot_count);
+        if (t0 >= nslots)
+            return;             /* the grid is sized for the worst padding */
+    }
+    /* a sorted tile is one pattern's: take it from the tile's first stripe
+     * (never padding: runs are padded at their end) */
+    const uint64_t tp = SLOTS ? slot_stripe<SLOTS>(a, t0, nslots) : t0;
+    const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp), lane, lds + k * (T * ECD_CHUNK));
 
     /* stage: every wave instruction (global_load_lds_dwordx4) fills 1 KiB of
      * LDS linearly = planes b, b+1 of input p for the tile's 8 stripes (T=8)
@@ -440,8 +474,8 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             break;
         const u32 el = (ins * 64 + lane) % (T * 32); /* piece within input p */
         const u32 s = (el >> 2) % T;
-        const uint64_t st = t0 + s;
-        if (st < a.nstripes) {
+        const uint64_t st = slot_stripe<SLOTS>(a, t0 + s, nslots);
+        if (st != kNoSlot) {
             const u32 src = pw.byte(a, p);
             const uint8_t *g = a.in_base[src] + st * a.in_stride + ((el >> 2) / T) * 64u +
                                (el & 3u) * 16u;
@@ -487,8 +521,8 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             else
                 ecgf::mul_xor_rt<CW, CSE>(c, acc, y);
         }
-        const uint64_t ost = t0 + s;
-        if (ost < a.nstripes)
+        const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
+        if (ost != kNoSlot)
             store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
     }
 }
@@ -593,66 +627,79 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
     }
 }
 
-/* Mixed-pattern combine for pattern groups smaller than a tile (1, 2 or 4
- * stripes: a batch of small reads, each with its own set of live bricks).
- * The 8 stripes of a wave may then need up to 8 different decode matrices,
- * and the compare-tree multiply needs a wave-uniform coefficient.  So the
- * wave runs a waterfall over its pattern ids: each pass takes the id of the
- * first live lane, and the lanes holding that id decode their stripe with
- * uniform coefficients while the others wait.  One dword per plane per lane
- * (16 lanes per stripe, 4 stripes per wave) bounds a wave at 4 passes: with
- * 2 dwords (8 stripes per wave) 1-stripe groups took up to 8 passes of twice
- * the code.  No LDS tile (its staging needs one src[] per tile): inputs are
- * read straight from HBM and re-read per output row from L2.  Correctness path
- * for a shape the tile kernels cannot take; groups of >= 8 stripes use
- * ec_combine. */
-template <bool PG>
-__device__ __forceinline__ u32 fine_word(const CombineArgs &a, u32 i)
+/* Counting sort of the stripes of a mixed call by pattern id, for pattern
+ * groups of 1, 2 or 4 stripes, so the tile kernel gets 8 stripes of one
+ * pattern per tile.  Each pattern's run is padded to a multiple of 8 slots
+ * (kNoStripe), so tiles never straddle two patterns:
+ *   ec_slots_count    per-pattern stripe counts (LDS histogram per block)
+ *   ec_slots_scan     padded run offsets, the slot total (one block)
+ *   ec_slots_scatter  slot of every stripe (LDS ranks + one global atomic
+ *                     per block and pattern)
+ * Order within a run follows the blocks' atomics; any order decodes the same
+ * bytes.  Workspace: counts[256], cursors[256], total, slots. */
+constexpr u32 kSlotBlock = 256, kSlotPerThread = 8;
+
+__device__ __forceinline__ u32 clamp_pattern(const CombineArgs &a, uint64_t st)
 {
-    if constexpr (PG)
-        return __builtin_amdgcn_readfirstlane(a.patg[i]);
-    else
-        return a.pat[i];
+    const u32 id = a.group_pattern[st >> a.group_shift];
+    return id < a.npatterns ? id : a.npatterns - 1u;
 }
 
-template <bool PG>
-__global__ __launch_bounds__(256) void ec_combine_fine(const CombineArgs a)
+__global__ __launch_bounds__(kSlotBlock) void ec_slots_count(const CombineArgs a, u32 *counts)
 {
-    const uint64_t gtid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    const uint64_t st = gtid >> 4;            /* 16 lanes per stripe, 1 dword per plane */
-    const u32 cc = threadIdx.x & 15u;
-    if (st >= a.nstripes)
-        return;
-    u32 id = a.group_pattern[st >> a.group_shift];
-    if (id >= a.npatterns)                    /* clamp, as tile_pattern */
-        id = a.npatterns - 1u;
-    for (;;) {
-        const u32 cur = __builtin_amdgcn_readfirstlane(id);
-        if (id != cur)
-            continue;
-        const u32 pb = cur * a.pwords;
-        for (u32 r = 0; r < a.rows; ++r) {
-            u32 acc[8][1], y[8][1];
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-                acc[b][0] = 0;
-            for (u32 p = 0; p < a.k; ++p) {
-                const u32 cw = fine_word<PG>(a, pb + a.kw * (1 + r) + (p >> 2));
-                const u32 c = __builtin_amdgcn_readfirstlane((cw >> ((p & 3u) * 8u)) & 0xFFu);
-                if (c == 0)                   /* ec-code-c.c:11666-11676 */
-                    continue;
-                const u32 sw = fine_word<PG>(a, pb + (p >> 2));
-                const u32 src = __builtin_amdgcn_readfirstlane((sw >> ((p & 3u) * 8u)) & 0xFFu);
-                const uint8_t *g = a.in_base[src] + st * a.in_stride + cc * 4u;
-#pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    load_plane<1>(g + b * 64, y[b]);
-                ecgf::mul_xor_rt<1>(c, acc, y);
-            }
-            store_chunk<1, false>(a.out_base[r] + st * a.out_stride + cc * 4u, acc);
-        }
-        break;
+    __shared__ u32 h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kSlotBlock * kSlotPerThread;
+    for (u32 i = 0; i < kSlotPerThread; ++i) {
+        const uint64_t st = base + i * kSlotBlock + threadIdx.x;
+        if (st < a.nstripes)
+            atomicAdd(&h[clamp_pattern(a, st)], 1u);
     }
+    __syncthreads();
+    if (h[threadIdx.x])
+        atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void ec_slots_scan(const u32 *counts, u32 *cursors, u32 *total)
+{
+    __shared__ u32 v[256];
+    const u32 t = threadIdx.x;
+    v[t] = (counts[t] + 7u) & ~7u;
+    __syncthreads();
+    for (u32 o = 1; o < 256; o <<= 1) {     /* Hillis-Steele inclusive scan */
+        const u32 x = t >= o ? v[t - o] : 0u;
+        __syncthreads();
+        v[t] += x;
+        __syncthreads();
+    }
+    cursors[t] = v[t] - ((counts[t] + 7u) & ~7u);
+    if (t == 255)
+        *total = v[255];
+}
+
+__global__ __launch_bounds__(kSlotBlock) void ec_slots_scatter(const CombineArgs a, u32 *cursors,
+                                                               u32 *slots)
+{
+    __shared__ u32 h[256], basep[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kSlotBlock * kSlotPerThread;
+    u32 pat[kSlotPerThread], rank[kSlotPerThread];
+#pragma unroll
+    for (u32 i = 0; i < kSlotPerThread; ++i) {
+        const uint64_t st = base + i * kSlotBlock + threadIdx.x;
+        pat[i] = st < a.nstripes ? clamp_pattern(a, st) : 256u;
+        rank[i] = pat[i] < 256u ? atomicAdd(&h[pat[i]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (h[threadIdx.x])
+        basep[threadIdx.x] = atomicAdd(&cursors[threadIdx.x], h[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (u32 i = 0; i < kSlotPerThread; ++i)
+        if (pat[i] < 256u)
+            slots[basep[pat[i]] + rank[i]] = (u32)(base + i * kSlotBlock + threadIdx.x);
 }
 
 template <int TS>
