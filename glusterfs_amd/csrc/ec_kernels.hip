@@ -280,9 +280,9 @@ int launch_combine_slots(hipStream_t s, const CombineArgs &a0)
     }
     if (rc == 0) {
         if (a.k <= 4)
-            rc = launch_combine<4, 1, 8, 8, NTS, false, false, true>(s, a);
+            rc = launch_combine<4, 1, 8, 8, NTS, true, true, true>(s, a);
         else if (a.k <= 8)
-            rc = launch_combine<8, 1, 8, 8, NTS, false, true, true>(s, a);
+            rc = launch_combine<8, 1, 8, 8, NTS, true, true, true>(s, a);
         else
             rc = launch_combine<16, 1, 16, 16, NTS, true, true, true>(s, a);
     }
@@ -308,21 +308,17 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
     if (a.group_pattern && a.group_shift < 3)
         return launch_combine_slots<NTS>(s, a);
     /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
-    /* the jump-table multiply (r02, profiles/kbench_r02d.log): 16+4 decode
-     * 0.571 -> 0.680 of 8 TB/s (the compare tree's scalar work was the
-     * bound), 8+4 mixed 0.701 -> 0.717, 8+4 single pattern a tie, 4+2 a
-     * loss (0.741 -> 0.685), so 4+2 keeps the switch */
+    /* The multiply dispatch is the jump table (ec_gf8_asm.h) for every k:
+     * same-box A/B through this launcher, EC_MI355X_JT=0/1 alternating
+     * (profiles/ab_jt_r02f.log): 8+4 decode 1 GiB 0.440 -> 0.392-0.403 ms,
+     * 16+4 mixed 64 masks 0.591-0.608 -> 0.505 ms, 4+2 0x3C 0.365 -> 0.360,
+     * 8+4 64K-stripe batches and 8+4 mixed ties.  EC_MI355X_JT=0 keeps the
+     * compiler's switch for A/Bs. */
+    const bool sw = jt == 0;
     if (a.k <= 4)
-        return jt == 1 ? launch_combine<4, 1, 8, 8, NTS, true, true>(s, a)
-                       : launch_combine<4, 1, 8, 8, NTS, false, false>(s, a);
+        return sw ? launch_combine<4, 1, 8, 8, NTS, false, false>(s, a)
+                  : launch_combine<4, 1, 8, 8, NTS, true, true>(s, a);
     if (a.k <= 8) {
-        if (jt >= 0) {
-            if (a.rows > 4 && a.nstripes <= (1u << 17))
-                return jt ? launch_combine<8, 1, 16, 8, NTS, true, true>(s, a)
-                          : launch_combine<8, 1, 16, 8, NTS, false, false>(s, a);
-            return jt ? launch_combine<8, 1, 4, 8, NTS, true, true>(s, a)
-                      : launch_combine<8, 1, 4, 8, NTS, false, false>(s, a);
-        }
         /* Full decodes (rows > 4) of up to 128K stripes use 16-wave blocks:
          * 64K-stripe batches (BASELINE configs[2]) 99.5 -> 91 us for 0xFF0,
          * 108 -> 100 us for 0xEB5, same box, alternating libraries; at 1 GiB
@@ -330,11 +326,13 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
          * (profiles/kbench_r01_ts_*.log, ab_r01_nw16.log).  Heal-shaped
          * calls (rows <= 4) keep 4 waves. */
         if (a.rows > 4 && a.nstripes <= (1u << 17))
-            return launch_combine<8, 1, 16, 8, NTS, false, true>(s, a);
-        return launch_combine<8, 1, 4, 8, NTS, false, true>(s, a);
+            return sw ? launch_combine<8, 1, 16, 8, NTS, false, false>(s, a)
+                      : launch_combine<8, 1, 16, 8, NTS, true, true>(s, a);
+        return sw ? launch_combine<8, 1, 4, 8, NTS, false, false>(s, a)
+                  : launch_combine<8, 1, 4, 8, NTS, true, true>(s, a);
     }
-    return jt == 0 ? launch_combine<16, 1, 16, 16, NTS, false, false>(s, a)
-                   : launch_combine<16, 1, 16, 16, NTS, true, true>(s, a);
+    return sw ? launch_combine<16, 1, 16, 16, NTS, false, false>(s, a)
+              : launch_combine<16, 1, 16, 16, NTS, true, true>(s, a);
 }
 
 /* pack, then launch; -E2BIG from the packer means "use a device table" */

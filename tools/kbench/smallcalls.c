@@ -158,12 +158,15 @@ static int cell(ec_matrix_list_t *list, uint32_t k, uint32_t n, uintptr_t mask, 
     qsort(all, nl, sizeof(double), cmpd);
     const double busy = secs; /* each thread ran ~secs of back-to-back calls */
     (void)el;
+    ec_method_stats_t st;
+    ec_method_get_stats(&st);
     printf("%2u+%-2u %s %-10s %5zu KiB x %2d thr: %8.2f GB/s user  %8.0f calls/s  "
-           "p50 %7.1f us  p99 %7.1f us  %s\n",
+           "p50 %7.1f us  p99 %7.1f us  %s  [%s: gpu %llu cpu %llu]\n",
            k, n - k, decode ? "dec" : "enc", registered ? "registered" : "pageable", size >> 10,
            threads, (double)calls * size / busy / 1e9, calls / busy,
            nl ? all[nl / 2] * 1e6 : 0.0, nl ? all[(long)(nl * 0.99)] * 1e6 : 0.0,
-           bad ? "MISMATCH" : "ok");
+           bad ? "MISMATCH" : "ok", ec_method_engine(list), (unsigned long long)st.gpu_calls,
+           (unsigned long long)st.cpu_calls);
     fflush(stdout);
     free(all);
     if (registered) {
@@ -176,10 +179,10 @@ static int cell(ec_matrix_list_t *list, uint32_t k, uint32_t n, uintptr_t mask, 
 int main(int argc, char **argv)
 {
     const double secs = argc > 1 ? atof(argv[1]) : 1.0;
-    if (argc > 6) { /* one cell: secs k dec reg KiB threads */
+    if (argc > 6) { /* one cell: secs k dec reg KiB threads [gen] */
         const uint32_t k = atoi(argv[2]), n = k + k / 2;
         ec_matrix_list_t list;
-        if (ec_method_init(NULL, &list, k, n, 2 * n, "auto") != 0)
+        if (ec_method_init(NULL, &list, k, n, 2 * n, argc > 7 ? argv[7] : "auto") != 0)
             return 1;
         const size_t sz = ((size_t)atoi(argv[5]) << 10) / (512 * k) * (512 * k);
         const int bad = cell(&list, k, n, ((1u << n) - 1) & ~((1u << (n - k)) - 1), sz,
