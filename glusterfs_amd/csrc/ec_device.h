@@ -106,6 +106,10 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes,
  * (or no device exists): the caller should code on its own CPU thread. */
 int ecd_host_busy(uint64_t limit);
 
+/* 1 when [p, p + n) lies in pinned, device-mapped host memory (the
+ * zero-copy path), 0 for pageable memory or without a device. */
+int ecd_host_mapped(const void *p, size_t n);
+
 /* Test hook: the next n host-buffer submissions fail with -EIO before
  * touching a device (exercises the CPU fallback). */
 void ecd_inject_faults(uint32_t n);

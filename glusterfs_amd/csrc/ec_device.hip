@@ -956,6 +956,11 @@ int ecd_host_busy(uint64_t limit)
     return 1;
 }
 
+int ecd_host_mapped(const void *p, size_t n)
+{
+    return ecd_device_count() > 0 && mapped(p, n) != nullptr;
+}
+
 void ecd_inject_faults(uint32_t n)
 {
     g_inject_faults.store(n);

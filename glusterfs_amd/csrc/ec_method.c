@@ -245,13 +245,25 @@ ec_method_inject_device_faults(uint32_t count)
 }
 
 /* Host-buffer crossover.  GlusterFS codes one fop per
- * call: 128 KiB FUSE writes (fuse-bridge.c:5179) up to 4 MiB heal blocks
- * (ec-heal.c:2063-2068), on several threads at once.  A call whose bytes
- * (read + written) are below EC_CPU_BELOW_KB runs on the calling thread, as
- * a PCIe round trip costs more; so does a call that finds every GPU with
- * EC_GPU_INFLIGHT_MB or more of host-buffer work in flight, so concurrent
- * callers use the CPU and the GPUs together.  Defaults from the smallcalls
- * measurements on MI355X. */
+ * call -- 128 KiB FUSE writes (fuse-bridge.c:5179) up to 4 MiB heal blocks
+ * (ec-heal.c:2063-2068) -- on several threads at once, and each call can run
+ * on its own thread (the CPU engine) or be shipped over PCIe.  Measured on
+ * the MI355X hosts (EPYC 9575F, AVX-512; tools/kbench/xover_cells.sh,
+ * profiles/xover_r02g.log): the CPU engine codes 4+2 calls of 128 KiB-16 MiB
+ * at 19-46 GB/s per thread while a GPU's host-buffer path reaches 3-22 GB/s
+ * per call (launch + PCIe latency, and for pageable buffers a CPU staging
+ * copy that costs as much as coding); only decodes of wide codes (k >= 8,
+ * ~k/4 times the XOR work of 4+2) and calls past the caches favour the GPU.
+ * So a host call goes to the GPU when
+ *   - it is a decode-type call (decode, mixed, heal) with k >= 8 moving at
+ *     least EC_GPU_HEAVY_KB (default 1 MiB) from device-mapped buffers or
+ *     EC_GPU_HEAVY_PAGEABLE_KB (8 MiB) from pageable ones, or
+ *   - it moves at least EC_GPU_LIGHT_MB (32 MiB; encodes and narrow decodes:
+ *     past the caches the CPU streams at ~15 GB/s per thread, a pinned
+ *     4+2 call over PCIe at 33-42),
+ * and the least-loaded host GPU has less than EC_GPU_INFLIGHT_MB (16 MiB) of
+ * host-buffer work in flight; concurrent callers then spread over the GPUs
+ * and the CPU.  EC_CPU_BELOW_KB (0 = off) forces calls below it to the CPU. */
 static uint64_t
 env_u64(const char *name, uint64_t dflt)
 {
@@ -265,26 +277,55 @@ env_u64(const char *name, uint64_t dflt)
     return (end && *end == 0) ? (uint64_t)v : dflt;
 }
 
-static uint64_t ecm_cpu_below, ecm_gpu_inflight;
+static uint64_t ecm_cpu_below, ecm_gpu_inflight, ecm_heavy_mapped, ecm_heavy_pageable,
+    ecm_light;
 static pthread_once_t ecm_xover_once = PTHREAD_ONCE_INIT;
 
 static void
 xover_init(void)
 {
-    ecm_cpu_below = env_u64("EC_CPU_BELOW_KB", 1024) << 10;
-    ecm_gpu_inflight = env_u64("EC_GPU_INFLIGHT_MB", 64) << 20;
+    ecm_cpu_below = env_u64("EC_CPU_BELOW_KB", 0) << 10;
+    ecm_gpu_inflight = env_u64("EC_GPU_INFLIGHT_MB", 16) << 20;
+    ecm_heavy_mapped = env_u64("EC_GPU_HEAVY_KB", 1024) << 10;
+    ecm_heavy_pageable = env_u64("EC_GPU_HEAVY_PAGEABLE_KB", 8192) << 10;
+    ecm_light = env_u64("EC_GPU_LIGHT_MB", 32) << 20;
 }
 
-/* 1: code this host-buffer call on the CPU engine */
+enum { ECM_LIGHT = 0, ECM_HEAVY = 1 };
+
+/* 1: code this host-buffer call on the CPU engine.  `bytes`: read + written;
+ * `heavy`: decode-type call with k >= 8; `mapped`: every buffer is pinned,
+ * device-mapped host memory (zero-copy over PCIe). */
 static int
-route_cpu(const ecm_ctx_t *ctx, uint64_t bytes)
+route_cpu(const ecm_ctx_t *ctx, uint64_t bytes, int heavy, int mapped)
 {
+    uint64_t min;
+
     if (ctx->engine == ECM_ENGINE_CPU)
         return 1;
     pthread_once(&ecm_xover_once, xover_init);
     if (bytes < ecm_cpu_below)
         return 1;
+    if (heavy == ECM_HEAVY && ctx->k >= 8)
+        min = mapped ? ecm_heavy_mapped : ecm_heavy_pageable;
+    else
+        min = ecm_light;
+    if (bytes < min)
+        return 1;
     return ecd_host_busy(ecm_gpu_inflight);
+}
+
+/* 1 when every non-NULL buffer of b[0..n) (len bytes each) is pinned,
+ * device-mapped host memory */
+static int
+all_mapped(const void *const *b, uint32_t n, uint64_t len)
+{
+    uint32_t i;
+
+    for (i = 0; i < n; i++)
+        if (b[i] && !ecd_host_mapped(b[i], len))
+            return 0;
+    return 1;
 }
 
 /* A failed device submission for host buffers: log once, count, and let
@@ -764,7 +805,10 @@ host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
     const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n);
     int rc;
 
-    if (!route_cpu(ctx, bytes)) {
+    if (!route_cpu(ctx, bytes, ECM_LIGHT,
+                   ecd_host_mapped(in, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k) &&
+                       all_mapped((const void *const *)out, ctx->n,
+                                  nstripes * EC_METHOD_CHUNK_SIZE))) {
         rc = ecd_encode_host(0, ctx->k, ctx->n, nstripes, in, out, ctx->enc_pat);
         if (!gpu_failed(rc)) {
             if (rc == 0)
@@ -785,11 +829,15 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
             const uint8_t *pats, const uint8_t *gp, uint32_t shift)
 {
     const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (k + rows);
+    const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE;
     ecd_combine_desc_t d;
     uint32_t f, r;
     int rc;
 
-    if (!route_cpu(ctx, bytes)) {
+    if (!route_cpu(ctx, bytes, ECM_HEAVY,
+                   all_mapped(frags, nfrags, fl) &&
+                       (outs ? all_mapped((const void *const *)outs, rows, fl)
+                             : ecd_host_mapped(out, fl * rows)))) {
         rc = ecd_decode_host(0, k, rows, nstripes, nfrags, frags, out, outs, npat, pats, gp,
                              shift);
         if (!gpu_failed(rc)) {
@@ -1158,7 +1206,7 @@ ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iove
     }
     segp[ns] = ts;
     segl[ns++] = nst * S - b2;
-    if (!route_cpu(ctx, nst * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n))) {
+    if (!route_cpu(ctx, nst * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n), ECM_LIGHT, 0)) {
         c = ecd_encode_host_gather(0, ctx->k, ctx->n, nst, ns, segp, segl, out, ctx->enc_pat);
         if (!gpu_failed(c)) {
             if (c == 0)

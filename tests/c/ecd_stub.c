@@ -36,3 +36,4 @@ int ecd_host_register(void *p, size_t b) { (void)p; (void)b; return -ENODEV; }
 int ecd_host_unregister(void *p) { (void)p; return -ENODEV; }
 int ecd_host_busy(uint64_t l) { (void)l; return 1; }
 void ecd_inject_faults(uint32_t n) { (void)n; }
+int ecd_host_mapped(const void *p, size_t n) { (void)p; (void)n; return 0; }

@@ -103,32 +103,47 @@ import json, sys
 import numpy as np
 sys.path[:0] = [sys.argv[1], sys.argv[1] + "/oracle"]
 import glusterfs_amd as g, oracle as O
-k, n = 4, 6
 res = {}
-with g.ECMatrixList(k, n) as L:
-    for name, nst in (("small", 64), ("large", 4096)):      # 128 KiB / 8 MiB of user data
-        data = np.random.default_rng(nst).integers(0, 256, 512 * k * nst, dtype=np.uint8)
+def run(name, k, n, op, user):
+    nst = user // (512 * k)
+    data = np.random.default_rng(nst).integers(0, 256, 512 * k * nst, dtype=np.uint8)
+    with g.ECMatrixList(k, n) as L:
+        frags = O.encode(k, n, data)
         s0 = g.stats()
-        outs = [np.zeros(512 * nst, np.uint8) for _ in range(n)]
-        L.encode_batch(nst, data, outs)
+        if op == "enc":
+            outs = [np.zeros(512 * nst, np.uint8) for _ in range(n)]
+            L.encode_batch(nst, data, outs)
+            ok = all(np.array_equal(a, b) for a, b in zip(outs, frags))
+        else:
+            rows = list(range(n - k + 1, n + 1))
+            out = np.zeros(data.size, np.uint8)
+            L.decode(512 * nst, sum(1 << (r - 1) for r in rows), rows,
+                     [frags[r - 1] for r in rows], out)
+            ok = bool(np.array_equal(out, data))
         s1 = g.stats()
-        ok = all(np.array_equal(a, b) for a, b in zip(outs, O.encode(k, n, data)))
-        res[name] = dict(gpu=s1["gpu_calls"] - s0["gpu_calls"],
-                         cpu=s1["cpu_calls"] - s0["cpu_calls"], ok=ok)
+    res[name] = dict(gpu=s1["gpu_calls"] - s0["gpu_calls"],
+                     cpu=s1["cpu_calls"] - s0["cpu_calls"], ok=ok)
+run("enc4+2_128K", 4, 6, "enc", 128 << 10)
+run("enc4+2_8M", 4, 6, "enc", 8 << 20)
+run("dec8+4_16M", 8, 12, "dec", 16 << 20)
+run("enc4+2_64M", 4, 6, "enc", 64 << 20)
 print("XOVER " + json.dumps(res))
 '''
 
 
 def test_crossover_defaults():
-    """Default thresholds (no test overrides): a 128 KiB FUSE-sized call is
-    coded on the calling thread, an 8 MiB one on the GPU."""
+    """Default thresholds (no test overrides, DESIGN.md 1.1): FUSE-sized and
+    cache-sized encodes on the calling thread, a 16 MiB 8+4 decode (pageable)
+    and a 64 MiB encode on the GPU."""
     env = {k: v for k, v in os.environ.items()
-           if k not in ("EC_CPU_BELOW_KB", "EC_GPU_INFLIGHT_MB")}
+           if not (k.startswith("EC_GPU_") or k.startswith("EC_CPU_"))}
     env["EC_MI355X_QUIET"] = "1"
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.dirname(HERE)], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("XOVER ")][0]
     res = json.loads(line[6:])
-    assert res["small"] == dict(gpu=0, cpu=1, ok=True), res
-    assert res["large"] == dict(gpu=1, cpu=0, ok=True), res
+    assert res["enc4+2_128K"] == dict(gpu=0, cpu=1, ok=True), res
+    assert res["enc4+2_8M"] == dict(gpu=0, cpu=1, ok=True), res
+    assert res["dec8+4_16M"] == dict(gpu=1, cpu=0, ok=True), res
+    assert res["enc4+2_64M"] == dict(gpu=1, cpu=0, ok=True), res

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -u
 mkdir -p gpurun_out
-TAG=${TAG:-r02g}
+TAG=${TAG:-r02h}
 run() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
   echo "[$(date +%T)] start $name"
@@ -11,7 +11,7 @@ run() {  # name timeout cmd...
   if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
 }
 run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread
-run bench 700 python -u bench.py
-run xover 400 bash tools/kbench/xover_cells.sh ${TAG}_xover_cells
-run profile 900 bash tools/profile.sh $TAG dec:4+2:3C 1 enc:4+2 1 dec:8+4:FF0 0.25 enc:8+4 0.25 dec:16+4:FFFF0 1 enc:16+4 2 mixed:8+4 1 mixed:8+4:16:1 1 heal:8+4 1
+run xover 400 bash tools/kbench/xover_cells.sh ${TAG}_xover_pageable
+run xover_reg 400 env REG=1 bash tools/kbench/xover_cells.sh ${TAG}_xover_registered
+run e2e 400 bash tools/kbench/e2e_sweep.sh ${TAG}_e2e
 du -sh gpurun_out

@@ -180,7 +180,7 @@ int main(int argc, char **argv)
 {
     const double secs = argc > 1 ? atof(argv[1]) : 1.0;
     if (argc > 6) { /* one cell: secs k dec reg KiB threads [gen] */
-        const uint32_t k = atoi(argv[2]), n = k + k / 2;
+        const uint32_t k = atoi(argv[2]), n = k == 16 ? 20 : k + k / 2;
         ec_matrix_list_t list;
         if (ec_method_init(NULL, &list, k, n, 2 * n, argc > 7 ? argv[7] : "auto") != 0)
             return 1;

@@ -14,7 +14,7 @@ while [ $# -ge 2 ]; do
   CFG=$1; GIB=$2; shift 2
   NAME=$(echo "$CFG" | tr ':+' '_p')
   for PASS in trace FETCH_SIZE WRITE_SIZE; do
-    if [ $PASS = trace ]; then ARGS="--kernel-trace --stats"; else ARGS="--kernel-trace --pmc $PASS"; fi
+    if [ $PASS = trace ]; then ARGS="--kernel-trace --stats"; else ARGS="--kernel-trace --kernel-include-regex ec_ --pmc $PASS"; fi
     echo "[$(date +%T)] $CFG $PASS"
     timeout -k 10 300 rocprofv3 $ARGS -d "$OUT/${NAME}_$PASS" -o run --output-format csv -- \
       python3 "$R/bench.py" --only "$CFG" --gib "$GIB" --steps 10 --warmup 2 \
@@ -22,5 +22,6 @@ while [ $# -ge 2 ]; do
     rc=$?
     echo "rc=$rc"; tail -2 "$OUT/${NAME}_$PASS.log"
     if [ $rc -ne 0 ]; then exit $rc; fi
+    python3 "$R/tools/prof_filter.py" "$OUT/${NAME}_$PASS"
   done
 done
