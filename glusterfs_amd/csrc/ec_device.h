@@ -102,9 +102,9 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes,
                     void *const *outs, uint32_t npatterns, const uint8_t *pats,
                     const uint8_t *group_pattern, uint32_t group_shift);
 
-/* 1 when every host-buffer device has at least `limit` bytes in flight
- * (or no device exists): the caller should code on its own CPU thread. */
-int ecd_host_busy(uint64_t limit);
+/* Bytes of host-buffer work in flight on the least-loaded host device
+ * (UINT64_MAX without a device): the queue a new call would wait behind. */
+uint64_t ecd_host_inflight(void);
 
 /* 1 when [p, p + n) lies in pinned, device-mapped host memory (the
  * zero-copy path), 0 for pageable memory or without a device. */

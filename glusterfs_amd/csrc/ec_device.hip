@@ -721,7 +721,7 @@ bool take_injected_fault()
 /* Run fn(dev, s0, s1) over a stripe-range partition; `align` keeps every
  * range boundary a multiple of it (pattern groups).  Bytes in flight are
  * tracked per device for placement and for the CPU crossover
- * (ecd_host_busy). */
+ * (ecd_host_inflight). */
 template <typename F>
 int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
 {
@@ -946,14 +946,14 @@ int ecd_decode_host(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, uint
     });
 }
 
-int ecd_host_busy(uint64_t limit)
+uint64_t ecd_host_inflight(void)
 {
     if (ecd_device_count() == 0)
-        return 1;
+        return UINT64_MAX;
+    uint64_t lo = UINT64_MAX;
     for (int i = 0; i < g_nhost; ++i)
-        if (g_inflight[g_host_devs[i]].load() < limit)
-            return 0;
-    return 1;
+        lo = std::min<uint64_t>(lo, g_inflight[g_host_devs[i]].load());
+    return lo;
 }
 
 int ecd_host_mapped(const void *p, size_t n)

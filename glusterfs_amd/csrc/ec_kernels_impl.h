@@ -435,7 +435,7 @@ __device__ __forceinline__ uint64_t slot_stripe(const CombineArgs &a, uint64_t s
  * stripes were sorted by pattern into 8-slot tiles (ec_slots_* kernels), and
  * the block reads its tile's stripes from the slot list. */
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, bool JT = false, bool SLOTS = false>
+          bool CSE = true, bool JT = false, bool SLOTS = false, int PU = 1>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -504,12 +504,17 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 #pragma unroll
             for (int w = 0; w < CW; ++w)
                 acc[b][w] = 0;
-        /* not unrolled: every copy of the loop body is a copy of the 255
-         * multiply programs (~54 KiB of code) */
-#pragma unroll 1
+        /* the row's coefficients as a 128-bit scalar shift register: one
+         * byte per input, 4 SALU per step instead of a select chain */
+        uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
+        /* PU = 1: not unrolled, as every copy of the body is a copy of the
+         * 255 multiply programs (~54 KiB of code) */
+#pragma unroll PU
         for (u32 p = 0; p < k; ++p) {
-            const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
-            const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
+            const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+            cl = (cl >> 8) | (ch << 56);
+            ch >>= 8;
             if (c == 0)                  /* ec-code-c.c:11666-11676 */
                 continue;
             const uint8_t *src = col + p * (T * ECD_CHUNK);
@@ -586,12 +591,17 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
 #pragma unroll
         for (int b = 0; b < 8; ++b)
             acc[b][0] = acc[b][1] = 0;
-        /* not unrolled: every copy of the loop body is a copy of the 255
-         * multiply programs (~54 KiB of code) */
+        /* the row's coefficients as a 128-bit scalar shift register: one
+         * byte per input, 4 SALU per step instead of a select chain */
+        uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
+        /* PU = 1: not unrolled, as every copy of the body is a copy of the
+         * 255 multiply programs (~54 KiB of code) */
 #pragma unroll 1
         for (u32 p = 0; p < k; ++p) {
-            const u32 wsel = p < 4 ? w0 : p < 8 ? w1 : p < 12 ? w2 : w3;
-            const u32 c = __builtin_amdgcn_readfirstlane((wsel >> ((p & 3u) * 8u)) & 0xFFu);
+            const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+            cl = (cl >> 8) | (ch << 56);
+            ch >>= 8;
             if (c == 0)                  /* ec-code-c.c:11666-11676 */
                 continue;
             const uint8_t *src = col + p * (T * ECD_CHUNK);

@@ -247,23 +247,26 @@ ec_method_inject_device_faults(uint32_t count)
 /* Host-buffer crossover.  GlusterFS codes one fop per
  * call -- 128 KiB FUSE writes (fuse-bridge.c:5179) up to 4 MiB heal blocks
  * (ec-heal.c:2063-2068) -- on several threads at once, and each call can run
- * on its own thread (the CPU engine) or be shipped over PCIe.  Measured on
- * the MI355X hosts (EPYC 9575F, AVX-512; tools/kbench/xover_cells.sh,
- * profiles/xover_r02g.log): the CPU engine codes 4+2 calls of 128 KiB-16 MiB
- * at 19-46 GB/s per thread while a GPU's host-buffer path reaches 3-22 GB/s
- * per call (launch + PCIe latency, and for pageable buffers a CPU staging
- * copy that costs as much as coding); only decodes of wide codes (k >= 8,
- * ~k/4 times the XOR work of 4+2) and calls past the caches favour the GPU.
- * So a host call goes to the GPU when
- *   - it is a decode-type call (decode, mixed, heal) with k >= 8 moving at
- *     least EC_GPU_HEAVY_KB (default 1 MiB) from device-mapped buffers or
- *     EC_GPU_HEAVY_PAGEABLE_KB (8 MiB) from pageable ones, or
- *   - it moves at least EC_GPU_LIGHT_MB (32 MiB; encodes and narrow decodes:
- *     past the caches the CPU streams at ~15 GB/s per thread, a pinned
- *     4+2 call over PCIe at 33-42),
- * and the least-loaded host GPU has less than EC_GPU_INFLIGHT_MB (16 MiB) of
- * host-buffer work in flight; concurrent callers then spread over the GPUs
- * and the CPU.  EC_CPU_BELOW_KB (0 = off) forces calls below it to the CPU. */
+ * on its own thread (the CPU engine) or be shipped to a GPU over PCIe.  The
+ * library estimates both completion times and takes the shorter:
+ *
+ *   CPU: user bytes / (rate(op) / k x isa factor x cache factor)
+ *        rate = EC_CPU_ENC_GBPS_K (180) for encodes, EC_CPU_DEC_GBPS_K (110)
+ *        for decode-type calls (decode, mixed, heal), i.e. 45 / 22 / 11 and
+ *        27 / 14 / 7 GB/s per thread for k = 4 / 8 / 16 with AVX-512 on the
+ *        MI355X hosts' EPYC 9575F (tools/kbench/xover_cells.sh,
+ *        profiles/xover_r02h_*.log); x0.7 with AVX2, x0.4 base x86-64;
+ *        x0.45 for calls moving more than 8 MiB (past the caches);
+ *   GPU: latency + (bytes in flight on the least-loaded host GPU + this
+ *        call) / rate, per call: 20 us and 30 GB/s of user data for pinned,
+ *        device-mapped buffers (zero copy), 60 us and 22 GB/s for pageable
+ *        ones (staging copies); EC_GPU_{PINNED,PAGEABLE}_{US,GBPS}.
+ *
+ * So FUSE-sized calls and light codes stay on the calling thread, wide-code
+ * decodes and large pinned calls go to the GPU, and concurrent callers queue
+ * on a GPU only while the queue is shorter than their own CPU time.
+ * EC_CPU_BELOW_KB forces calls below it to the CPU; EC_GPU_ALWAYS=1 sends
+ * every host call to the GPU (tests of the host kernels). */
 static uint64_t
 env_u64(const char *name, uint64_t dflt)
 {
@@ -277,42 +280,55 @@ env_u64(const char *name, uint64_t dflt)
     return (end && *end == 0) ? (uint64_t)v : dflt;
 }
 
-static uint64_t ecm_cpu_below, ecm_gpu_inflight, ecm_heavy_mapped, ecm_heavy_pageable,
-    ecm_light;
+static struct {
+    uint64_t cpu_below, enc_k, dec_k, pin_us, pin_gbps, page_us, page_gbps, always;
+} ecm_x;
 static pthread_once_t ecm_xover_once = PTHREAD_ONCE_INIT;
 
 static void
 xover_init(void)
 {
-    ecm_cpu_below = env_u64("EC_CPU_BELOW_KB", 0) << 10;
-    ecm_gpu_inflight = env_u64("EC_GPU_INFLIGHT_MB", 16) << 20;
-    ecm_heavy_mapped = env_u64("EC_GPU_HEAVY_KB", 1024) << 10;
-    ecm_heavy_pageable = env_u64("EC_GPU_HEAVY_PAGEABLE_KB", 8192) << 10;
-    ecm_light = env_u64("EC_GPU_LIGHT_MB", 32) << 20;
+    ecm_x.cpu_below = env_u64("EC_CPU_BELOW_KB", 0) << 10;
+    ecm_x.enc_k = env_u64("EC_CPU_ENC_GBPS_K", 180);
+    ecm_x.dec_k = env_u64("EC_CPU_DEC_GBPS_K", 110);
+    ecm_x.pin_us = env_u64("EC_GPU_PINNED_US", 20);
+    ecm_x.pin_gbps = env_u64("EC_GPU_PINNED_GBPS", 30);
+    ecm_x.page_us = env_u64("EC_GPU_PAGEABLE_US", 60);
+    ecm_x.page_gbps = env_u64("EC_GPU_PAGEABLE_GBPS", 22);
+    ecm_x.always = env_u64("EC_GPU_ALWAYS", 0);
 }
 
-enum { ECM_LIGHT = 0, ECM_HEAVY = 1 };
+enum { ECM_ENCODE = 0, ECM_DECODE = 1 };
 
-/* 1: code this host-buffer call on the CPU engine.  `bytes`: read + written;
- * `heavy`: decode-type call with k >= 8; `mapped`: every buffer is pinned,
- * device-mapped host memory (zero-copy over PCIe). */
+/* 1: code this host-buffer call on the CPU engine.  `user`: user bytes of
+ * the call; `moved`: bytes read + written; `op`: ECM_ENCODE / ECM_DECODE;
+ * `mapped`: every buffer is pinned, device-mapped host memory. */
 static int
-route_cpu(const ecm_ctx_t *ctx, uint64_t bytes, int heavy, int mapped)
+route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int mapped)
 {
-    uint64_t min;
+    static const double isa_f[] = {0.4, 0.7, 1.0};
+    double cpu_gbps, cpu_us, gpu_us, q;
+    uint64_t infl;
 
     if (ctx->engine == ECM_ENGINE_CPU)
         return 1;
     pthread_once(&ecm_xover_once, xover_init);
-    if (bytes < ecm_cpu_below)
+    if (ecm_x.always)
+        return 0;
+    if (moved < ecm_x.cpu_below)
         return 1;
-    if (heavy == ECM_HEAVY && ctx->k >= 8)
-        min = mapped ? ecm_heavy_mapped : ecm_heavy_pageable;
-    else
-        min = ecm_light;
-    if (bytes < min)
+    cpu_gbps = (double)(op == ECM_ENCODE ? ecm_x.enc_k : ecm_x.dec_k) / ctx->k *
+               isa_f[ctx->isa < 0 ? 0 : ctx->isa > 2 ? 2 : ctx->isa];
+    if (moved > (8u << 20))
+        cpu_gbps *= 0.45;
+    cpu_us = (double)user / (cpu_gbps * 1e3);
+    infl = ecd_host_inflight();
+    if (infl == UINT64_MAX)
         return 1;
-    return ecd_host_busy(ecm_gpu_inflight);
+    q = (double)infl * ((double)user / (double)moved); /* queued user bytes */
+    gpu_us = mapped ? (double)ecm_x.pin_us + (q + user) / ((double)ecm_x.pin_gbps * 1e3)
+                    : (double)ecm_x.page_us + (q + user) / ((double)ecm_x.page_gbps * 1e3);
+    return cpu_us <= gpu_us;
 }
 
 /* 1 when every non-NULL buffer of b[0..n) (len bytes each) is pinned,
@@ -805,7 +821,7 @@ host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
     const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n);
     int rc;
 
-    if (!route_cpu(ctx, bytes, ECM_LIGHT,
+    if (!route_cpu(ctx, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k, bytes, ECM_ENCODE,
                    ecd_host_mapped(in, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k) &&
                        all_mapped((const void *const *)out, ctx->n,
                                   nstripes * EC_METHOD_CHUNK_SIZE))) {
@@ -834,7 +850,7 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
     uint32_t f, r;
     int rc;
 
-    if (!route_cpu(ctx, bytes, ECM_HEAVY,
+    if (!route_cpu(ctx, fl * k, bytes, ECM_DECODE,
                    all_mapped(frags, nfrags, fl) &&
                        (outs ? all_mapped((const void *const *)outs, rows, fl)
                              : ecd_host_mapped(out, fl * rows)))) {
@@ -1206,7 +1222,8 @@ ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iove
     }
     segp[ns] = ts;
     segl[ns++] = nst * S - b2;
-    if (!route_cpu(ctx, nst * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n), ECM_LIGHT, 0)) {
+    if (!route_cpu(ctx, nst * EC_METHOD_CHUNK_SIZE * ctx->k,
+                   nst * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n), ECM_ENCODE, 0)) {
         c = ecd_encode_host_gather(0, ctx->k, ctx->n, nst, ns, segp, segl, out, ctx->enc_pat);
         if (!gpu_failed(c)) {
             if (c == 0)

@@ -34,6 +34,6 @@ void *ecd_host_alloc(size_t b) { (void)b; return NULL; }
 void ecd_host_free(void *p) { (void)p; }
 int ecd_host_register(void *p, size_t b) { (void)p; (void)b; return -ENODEV; }
 int ecd_host_unregister(void *p) { (void)p; return -ENODEV; }
-int ecd_host_busy(uint64_t l) { (void)l; return 1; }
+uint64_t ecd_host_inflight(void) { return UINT64_MAX; }
 void ecd_inject_faults(uint32_t n) { (void)n; }
 int ecd_host_mapped(const void *p, size_t n) { (void)p; (void)n; return 0; }

@@ -26,6 +26,4 @@ def oracle():
 # off for this process (read once, when the library first codes).  The
 # crossover itself is tested in a child process with the defaults
 # (tests/test_gpu_engine.py).
-for _k, _v in (("EC_CPU_BELOW_KB", "0"), ("EC_GPU_LIGHT_MB", "0"), ("EC_GPU_HEAVY_KB", "0"),
-               ("EC_GPU_HEAVY_PAGEABLE_KB", "0"), ("EC_GPU_INFLIGHT_MB", "1000000")):
-    os.environ.setdefault(_k, _v)
+os.environ.setdefault("EC_GPU_ALWAYS", "1")

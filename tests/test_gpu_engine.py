@@ -104,16 +104,22 @@ import numpy as np
 sys.path[:0] = [sys.argv[1], sys.argv[1] + "/oracle"]
 import glusterfs_amd as g, oracle as O
 res = {}
-def run(name, k, n, op, user):
+def run(name, k, n, op, user, pinned=False):
     nst = user // (512 * k)
     data = np.random.default_rng(nst).integers(0, 256, 512 * k * nst, dtype=np.uint8)
     with g.ECMatrixList(k, n) as L:
         frags = O.encode(k, n, data)
         s0 = g.stats()
         if op == "enc":
-            outs = [np.zeros(512 * nst, np.uint8) for _ in range(n)]
-            L.encode_batch(nst, data, outs)
+            pins = [g.PinnedArray(512 * nst) for _ in range(n)] if pinned else []
+            outs = [p.array for p in pins] or [np.zeros(512 * nst, np.uint8) for _ in range(n)]
+            src = g.PinnedArray(data.size) if pinned else None
+            if src is not None:
+                src.array[:] = data
+            L.encode_batch(nst, src.array if src is not None else data, outs)
             ok = all(np.array_equal(a, b) for a, b in zip(outs, frags))
+            for p in pins + ([src] if src is not None else []):
+                p.free()
         else:
             rows = list(range(n - k + 1, n + 1))
             out = np.zeros(data.size, np.uint8)
@@ -126,15 +132,15 @@ def run(name, k, n, op, user):
 run("enc4+2_128K", 4, 6, "enc", 128 << 10)
 run("enc4+2_8M", 4, 6, "enc", 8 << 20)
 run("dec8+4_16M", 8, 12, "dec", 16 << 20)
-run("enc4+2_64M", 4, 6, "enc", 64 << 20)
+run("enc4+2_64M_pinned", 4, 6, "enc", 64 << 20, pinned=True)
 print("XOVER " + json.dumps(res))
 '''
 
 
 def test_crossover_defaults():
-    """Default thresholds (no test overrides, DESIGN.md 1.1): FUSE-sized and
+    """Default cost model (no test overrides, DESIGN.md 1.1): FUSE-sized and
     cache-sized encodes on the calling thread, a 16 MiB 8+4 decode (pageable)
-    and a 64 MiB encode on the GPU."""
+    and a 64 MiB encode from pinned buffers on the GPU."""
     env = {k: v for k, v in os.environ.items()
            if not (k.startswith("EC_GPU_") or k.startswith("EC_CPU_"))}
     env["EC_MI355X_QUIET"] = "1"
@@ -146,4 +152,4 @@ def test_crossover_defaults():
     assert res["enc4+2_128K"] == dict(gpu=0, cpu=1, ok=True), res
     assert res["enc4+2_8M"] == dict(gpu=0, cpu=1, ok=True), res
     assert res["dec8+4_16M"] == dict(gpu=1, cpu=0, ok=True), res
-    assert res["enc4+2_64M"] == dict(gpu=1, cpu=0, ok=True), res
+    assert res["enc4+2_64M_pinned"] == dict(gpu=1, cpu=0, ok=True), res

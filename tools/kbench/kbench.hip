@@ -318,14 +318,13 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     add("TS1 NW8 NTS naive", ec_combine<K, 1, 8, false, true, 2, false, false>, 1, 8);
     add("TS1 NW16 NTS", ec_combine<K, 1, 16, false, true>, 1, 16);
     add("TS1 NW16 NTS naive", ec_combine<K, 1, 16, false, true, 2, false, false>, 1, 16);
-    add("TS1 NW16 NTS CW1", ec_combine<K, 1, 16, false, true, 1>, 1, 16);
     add("TS1 NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, true>, 1, 4);
     add("TS1 NW8 NTS jt", ec_combine<K, 1, 8, false, true, 2, false, true, true>, 1, 8);
     add("TS1 NW16 NTS jt", ec_combine<K, 1, 16, false, true, 2, false, true, true>, 1, 16);
-    if constexpr (K <= 8) {   /* CW = 4: 16 stripes per item, 16-stripe tiles */
-        add("TS2 NW8 NTS CW4", ec_combine<K, 2, 8, false, true, 4>, 2, 8);
-        add("TS2 NW16 NTS CW4", ec_combine<K, 2, 16, false, true, 4>, 2, 16);
-    }
+    add("TS1 NW4 NTS jt u4", ec_combine<K, 1, 4, false, true, 2, false, true, true, false, 4>, 1, 4);
+    add("TS1 NW8 NTS jt u4", ec_combine<K, 1, 8, false, true, 2, false, true, true, false, 4>, 1, 8);
+    add("TS1 NW16 NTS jt u4", ec_combine<K, 1, 16, false, true, 2, false, true, true, false, 4>, 1, 16);
+    add("TS1 NW16 NTS jt u2", ec_combine<K, 1, 16, false, true, 2, false, true, true, false, 2>, 1, 16);
 }
 
 template <int K, int N, typename KF>

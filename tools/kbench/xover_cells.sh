@@ -7,6 +7,7 @@
 set -u
 mkdir -p gpurun_out
 OUT=gpurun_out/${1:-xover}.log
+SECS=${SECS:-1.0}
 : > "$OUT"
 for k in 4 8 16; do
   for dec in 0 1; do
@@ -14,7 +15,7 @@ for k in 4 8 16; do
       for thr in 1 16; do
         for mode in gpu cpu auto; do
           case $mode in
-            gpu)  ENV="EC_GPU_LIGHT_MB=0 EC_GPU_HEAVY_KB=0 EC_GPU_HEAVY_PAGEABLE_KB=0 EC_GPU_INFLIGHT_MB=1000000"; GEN=auto ;;
+            gpu)  ENV="EC_GPU_ALWAYS=1"; GEN=auto ;;
             cpu)  ENV=""; GEN=avx ;;
             auto) ENV=""; GEN=auto ;;
           esac
