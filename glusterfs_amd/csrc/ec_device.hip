@@ -338,6 +338,9 @@ uint8_t *mapped(const void *p, size_t n)
 /* Per-device pipeline resources (pooled). */
 constexpr int kSlots = 2;
 
+/* Events are created with hipEventBlockingSync: a host call that waits for
+ * its batch sleeps instead of spinning a core (the client's CPU is shared
+ * with the CPU engine and the network stack). */
 struct Stage {
     int dev = -1;
     hipStream_t stream = nullptr;
@@ -381,7 +384,8 @@ Stage *acquire(int dev)
     bool ok = hipSetDevice(g_dev_ids[dev]) == hipSuccess &&
               hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess;
     for (int i = 0; ok && i < kSlots; ++i)
-        ok = hipEventCreateWithFlags(&s->done[i], hipEventDisableTiming) == hipSuccess;
+        ok = hipEventCreateWithFlags(&s->done[i], hipEventDisableTiming | hipEventBlockingSync) ==
+             hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         delete s;
@@ -460,7 +464,13 @@ int run_pipeline(Stage *s, uint64_t nbatches,
         prev_slot = slot;
     }
     drain();
-    ok(hipStreamSynchronize(s->stream));
+    /* wait by a blocking event, not a stream spin: the calling thread then
+     * sleeps while the GPU codes, and a GlusterFS client's other threads (or
+     * CPU-engine calls beside this one) keep the core */
+    if (rc == 0 && ok(hipEventRecord(s->done[0], s->stream)))
+        ok(hipEventSynchronize(s->done[0]));
+    else
+        (void)hipStreamSynchronize(s->stream);
     return rc;
 }
 

@@ -250,16 +250,16 @@ ec_method_inject_device_faults(uint32_t count)
  * on its own thread (the CPU engine) or be shipped to a GPU over PCIe.  The
  * library estimates both completion times and takes the shorter:
  *
- *   CPU: user bytes / (rate(op) / k x isa factor x cache factor)
- *        rate = EC_CPU_ENC_GBPS_K (180) for encodes, EC_CPU_DEC_GBPS_K (110)
- *        for decode-type calls (decode, mixed, heal), i.e. 45 / 22 / 11 and
- *        27 / 14 / 7 GB/s per thread for k = 4 / 8 / 16 with AVX-512 on the
- *        MI355X hosts' EPYC 9575F (tools/kbench/xover_cells.sh,
- *        profiles/xover_r02h_*.log); x0.7 with AVX2, x0.4 base x86-64;
- *        x0.45 for calls moving more than 8 MiB (past the caches);
+ *   CPU: user bytes / rate, rate = EC_CPU_ENC_GBPS_K2 (260) / (k + 2) for
+ *        encodes and EC_CPU_DEC_GBPS_K (110) / k for decode-type calls
+ *        (decode, mixed, heal): 43 / 26 / 14 and 27 / 14 / 7 GB/s per
+ *        thread for k = 4 / 8 / 16 with AVX-512 on the MI355X hosts' EPYC
+ *        9575F (tools/kbench/xover_cells.sh, profiles/xover_r02i_*.log);
+ *        x0.7 with AVX2, x0.4 base x86-64; calls moving more than 32 MiB
+ *        (past a CCD's L3) stream from DRAM: min(rate, 18) x 0.8;
  *   GPU: latency + (bytes in flight on the least-loaded host GPU + this
- *        call) / rate, per call: 20 us and 30 GB/s of user data for pinned,
- *        device-mapped buffers (zero copy), 60 us and 22 GB/s for pageable
+ *        call) / rate, per call: 20 us and 26 GB/s of user data for pinned,
+ *        device-mapped buffers (zero copy), 40 us and 14 GB/s for pageable
  *        ones (staging copies); EC_GPU_{PINNED,PAGEABLE}_{US,GBPS}.
  *
  * So FUSE-sized calls and light codes stay on the calling thread, wide-code
@@ -281,7 +281,7 @@ env_u64(const char *name, uint64_t dflt)
 }
 
 static struct {
-    uint64_t cpu_below, enc_k, dec_k, pin_us, pin_gbps, page_us, page_gbps, always;
+    uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, always;
 } ecm_x;
 static pthread_once_t ecm_xover_once = PTHREAD_ONCE_INIT;
 
@@ -289,12 +289,12 @@ static void
 xover_init(void)
 {
     ecm_x.cpu_below = env_u64("EC_CPU_BELOW_KB", 0) << 10;
-    ecm_x.enc_k = env_u64("EC_CPU_ENC_GBPS_K", 180);
+    ecm_x.enc_k2 = env_u64("EC_CPU_ENC_GBPS_K2", 260);
     ecm_x.dec_k = env_u64("EC_CPU_DEC_GBPS_K", 110);
     ecm_x.pin_us = env_u64("EC_GPU_PINNED_US", 20);
-    ecm_x.pin_gbps = env_u64("EC_GPU_PINNED_GBPS", 30);
-    ecm_x.page_us = env_u64("EC_GPU_PAGEABLE_US", 60);
-    ecm_x.page_gbps = env_u64("EC_GPU_PAGEABLE_GBPS", 22);
+    ecm_x.pin_gbps = env_u64("EC_GPU_PINNED_GBPS", 26);
+    ecm_x.page_us = env_u64("EC_GPU_PAGEABLE_US", 40);
+    ecm_x.page_gbps = env_u64("EC_GPU_PAGEABLE_GBPS", 14);
     ecm_x.always = env_u64("EC_GPU_ALWAYS", 0);
 }
 
@@ -317,10 +317,11 @@ route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int mappe
         return 0;
     if (moved < ecm_x.cpu_below)
         return 1;
-    cpu_gbps = (double)(op == ECM_ENCODE ? ecm_x.enc_k : ecm_x.dec_k) / ctx->k *
+    cpu_gbps = (op == ECM_ENCODE ? (double)ecm_x.enc_k2 / (ctx->k + 2)
+                                 : (double)ecm_x.dec_k / ctx->k) *
                isa_f[ctx->isa < 0 ? 0 : ctx->isa > 2 ? 2 : ctx->isa];
-    if (moved > (8u << 20))
-        cpu_gbps *= 0.45;
+    if (moved > (32u << 20))
+        cpu_gbps = (cpu_gbps < 18.0 ? cpu_gbps : 18.0) * 0.8;
     cpu_us = (double)user / (cpu_gbps * 1e3);
     infl = ecd_host_inflight();
     if (infl == UINT64_MAX)

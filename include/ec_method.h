@@ -137,8 +137,8 @@ int32_t ec_method_decode_batch(ec_matrix_list_t *list, uint64_t nstripes,
  * are all n fragment buffers (nstripes*512 bytes each; entries of bricks no
  * group reads may be NULL), group g = stripes [g*group_stripes,
  * (g+1)*group_stripes) is decoded from the k bricks in group_masks[g].
- * group_stripes is a power of two (groups of >= 8 stripes run the tiled
- * kernel; 1, 2 or 4 run a per-stripe kernel, several times slower).
+ * group_stripes is a power of two (groups of 1, 2 or 4 stripes are sorted
+ * by pattern into 8-stripe tiles on the device first).
  * out = nstripes*k*512 bytes.
  * Up to 256 distinct masks per call (-E2BIG beyond). */
 int32_t ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes,

@@ -131,7 +131,7 @@ def run(name, k, n, op, user, pinned=False):
                      cpu=s1["cpu_calls"] - s0["cpu_calls"], ok=ok)
 run("enc4+2_128K", 4, 6, "enc", 128 << 10)
 run("enc4+2_8M", 4, 6, "enc", 8 << 20)
-run("dec8+4_16M", 8, 12, "dec", 16 << 20)
+run("dec16+4_16M", 16, 20, "dec", 16 << 20)
 run("enc4+2_64M_pinned", 4, 6, "enc", 64 << 20, pinned=True)
 print("XOVER " + json.dumps(res))
 '''
@@ -139,7 +139,7 @@ print("XOVER " + json.dumps(res))
 
 def test_crossover_defaults():
     """Default cost model (no test overrides): FUSE-sized and
-    cache-sized encodes on the calling thread, a 16 MiB 8+4 decode (pageable)
+    cache-sized encodes on the calling thread, a 16 MiB 16+4 decode (pageable)
     and a 64 MiB encode from pinned buffers on the GPU."""
     env = {k: v for k, v in os.environ.items()
            if not (k.startswith("EC_GPU_") or k.startswith("EC_CPU_"))}
@@ -151,5 +151,5 @@ def test_crossover_defaults():
     res = json.loads(line[6:])
     assert res["enc4+2_128K"] == dict(gpu=0, cpu=1, ok=True), res
     assert res["enc4+2_8M"] == dict(gpu=0, cpu=1, ok=True), res
-    assert res["dec8+4_16M"] == dict(gpu=1, cpu=0, ok=True), res
+    assert res["dec16+4_16M"] == dict(gpu=1, cpu=0, ok=True), res
     assert res["enc4+2_64M_pinned"] == dict(gpu=1, cpu=0, ok=True), res

@@ -1,0 +1,18 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+TAG=${TAG:-r02j}
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "[$(date +%T)] start $name"
+  timeout -k 10 "$to" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"; tail -3 "gpurun_out/${TAG}_$name.log" | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+run affinity 120 python3 -u tools/affinity_probe.py
+run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread
+run xover 500 env SECS=0.7 bash tools/kbench/xover_cells.sh ${TAG}_xover_pageable
+run xover_reg 500 env SECS=0.7 REG=1 bash tools/kbench/xover_cells.sh ${TAG}_xover_registered
+run bench_2rank 600 env EC_BENCH_BACKEND=gloo EC_BENCH_DEVICE=0 python -u bench.py --gpus 2 --steps 5 --warmup 1
+du -sh gpurun_out
