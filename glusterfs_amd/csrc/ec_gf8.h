@@ -190,12 +190,15 @@ __device__ __forceinline__ void mul_xor_rt(u32 c, u32 (&acc)[8][W], const u32 (&
  * per lane: a jump through a PC-relative table into the searched program
  * for c (ec_gf8_asm.h, generated).  Replaces the switch above where the
  * compare tree's scalar work bounds the kernel. */
-template <int W>
+template <int W, int ALIGN = 0>
 __device__ __forceinline__ void mul_xor_jt(u32 c, u32 (&acc)[8][W], const u32 (&x)[8][W])
 {
     static_assert(W == 2, "the assembly bodies are generated for 2 dwords per lane");
     u32 t[ECGF_ASM_TEMPS][2];
-    ECGF_ASM_DISPATCH_W2(acc, x, t, c);
+    if constexpr (ALIGN)
+        ECGF_ASM_DISPATCH_W2_A32(acc, x, t, c);  /* bodies on 32-byte boundaries */
+    else
+        ECGF_ASM_DISPATCH_W2(acc, x, t, c);
 }
 
 } // namespace ecgf

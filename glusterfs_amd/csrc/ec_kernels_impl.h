@@ -431,11 +431,13 @@ __device__ __forceinline__ uint64_t slot_stripe(const CombineArgs &a, uint64_t s
  * one lane address serves all 8 planes of an input (ds_read2st64_b64 with
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
-/* SLOTS: mixed patterns with groups below a tile (1, 2, 4 stripes): the
+/* JT: 0 = the compiler's switch, 1 = the jump table of ec_gf8_asm.h, 2 = the
+ * same with 32-byte-aligned bodies.
+ * SLOTS: mixed patterns with groups below a tile (1, 2, 4 stripes): the
  * stripes were sorted by pattern into 8-slot tiles (ec_slots_* kernels), and
  * the block reads its tile's stripes from the slot list. */
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, bool JT = false, bool SLOTS = false, int PU = 1>
+          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -522,7 +524,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             for (int b = 0; b < 8; ++b)
                 load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
             if constexpr (JT && CW == 2)
-                ecgf::mul_xor_jt<CW>(c, acc, y);
+                ecgf::mul_xor_jt<CW, JT == 2>(c, acc, y);
             else
                 ecgf::mul_xor_rt<CW, CSE>(c, acc, y);
         }

@@ -256,11 +256,13 @@ ec_method_inject_device_faults(uint32_t count)
  *        thread for k = 4 / 8 / 16 with AVX-512 on the MI355X hosts' EPYC
  *        9575F (tools/kbench/xover_cells.sh, profiles/xover_r02i_*.log);
  *        x0.7 with AVX2, x0.4 base x86-64; calls moving more than 32 MiB
- *        (past a CCD's L3) stream from DRAM: min(rate, 18) x 0.8;
+ *        (past a CCD's L3) stream from DRAM: min(rate, 22) x 0.9;
  *   GPU: latency + (bytes in flight on the least-loaded host GPU + this
- *        call) / rate, per call: 20 us and 26 GB/s of user data for pinned,
- *        device-mapped buffers (zero copy), 40 us and 14 GB/s for pageable
- *        ones (staging copies); EC_GPU_{PINNED,PAGEABLE}_{US,GBPS}.
+ *        call) / rate, per call: 30 us and 26 GB/s of user data for pinned,
+ *        device-mapped buffers (zero copy); 40 us and 14 GB/s for pageable
+ *        ones (staging copies), 21 GB/s from 8 MiB of user data on (the copy
+ *        pool splits a call into 2 MiB pieces, so larger calls copy on more
+ *        threads); EC_GPU_{PINNED,PAGEABLE}_{US,GBPS}, EC_GPU_PAGEABLE_GBPS_L.
  *
  * So FUSE-sized calls and light codes stay on the calling thread, wide-code
  * decodes and large pinned calls go to the GPU, and concurrent callers queue
@@ -281,7 +283,7 @@ env_u64(const char *name, uint64_t dflt)
 }
 
 static struct {
-    uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, always;
+    uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, page_gbps_l, always;
 } ecm_x;
 static pthread_once_t ecm_xover_once = PTHREAD_ONCE_INIT;
 
@@ -291,10 +293,11 @@ xover_init(void)
     ecm_x.cpu_below = env_u64("EC_CPU_BELOW_KB", 0) << 10;
     ecm_x.enc_k2 = env_u64("EC_CPU_ENC_GBPS_K2", 260);
     ecm_x.dec_k = env_u64("EC_CPU_DEC_GBPS_K", 110);
-    ecm_x.pin_us = env_u64("EC_GPU_PINNED_US", 20);
+    ecm_x.pin_us = env_u64("EC_GPU_PINNED_US", 30);
     ecm_x.pin_gbps = env_u64("EC_GPU_PINNED_GBPS", 26);
     ecm_x.page_us = env_u64("EC_GPU_PAGEABLE_US", 40);
     ecm_x.page_gbps = env_u64("EC_GPU_PAGEABLE_GBPS", 14);
+    ecm_x.page_gbps_l = env_u64("EC_GPU_PAGEABLE_GBPS_L", 21);
     ecm_x.always = env_u64("EC_GPU_ALWAYS", 0);
 }
 
@@ -321,14 +324,17 @@ route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int mappe
                                  : (double)ecm_x.dec_k / ctx->k) *
                isa_f[ctx->isa < 0 ? 0 : ctx->isa > 2 ? 2 : ctx->isa];
     if (moved > (32u << 20))
-        cpu_gbps = (cpu_gbps < 18.0 ? cpu_gbps : 18.0) * 0.8;
+        cpu_gbps = (cpu_gbps < 22.0 ? cpu_gbps : 22.0) * 0.9;
     cpu_us = (double)user / (cpu_gbps * 1e3);
     infl = ecd_host_inflight();
     if (infl == UINT64_MAX)
         return 1;
     q = (double)infl * ((double)user / (double)moved); /* queued user bytes */
     gpu_us = mapped ? (double)ecm_x.pin_us + (q + user) / ((double)ecm_x.pin_gbps * 1e3)
-                    : (double)ecm_x.page_us + (q + user) / ((double)ecm_x.page_gbps * 1e3);
+                    : (double)ecm_x.page_us +
+                          (q + user) / ((double)(user >= (8u << 20) ? ecm_x.page_gbps_l
+                                                                    : ecm_x.page_gbps) *
+                                        1e3);
     return cpu_us <= gpu_us;
 }
 

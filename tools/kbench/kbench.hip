@@ -318,13 +318,14 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     add("TS1 NW8 NTS naive", ec_combine<K, 1, 8, false, true, 2, false, false>, 1, 8);
     add("TS1 NW16 NTS", ec_combine<K, 1, 16, false, true>, 1, 16);
     add("TS1 NW16 NTS naive", ec_combine<K, 1, 16, false, true, 2, false, false>, 1, 16);
-    add("TS1 NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, true>, 1, 4);
-    add("TS1 NW8 NTS jt", ec_combine<K, 1, 8, false, true, 2, false, true, true>, 1, 8);
-    add("TS1 NW16 NTS jt", ec_combine<K, 1, 16, false, true, 2, false, true, true>, 1, 16);
-    add("TS1 NW4 NTS jt u4", ec_combine<K, 1, 4, false, true, 2, false, true, true, false, 4>, 1, 4);
-    add("TS1 NW8 NTS jt u4", ec_combine<K, 1, 8, false, true, 2, false, true, true, false, 4>, 1, 8);
-    add("TS1 NW16 NTS jt u4", ec_combine<K, 1, 16, false, true, 2, false, true, true, false, 4>, 1, 16);
-    add("TS1 NW16 NTS jt u2", ec_combine<K, 1, 16, false, true, 2, false, true, true, false, 2>, 1, 16);
+    add("TS1 NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 1, 4);
+    add("TS1 NW8 NTS jt", ec_combine<K, 1, 8, false, true, 2, false, true, 1>, 1, 8);
+    add("TS1 NW16 NTS jt", ec_combine<K, 1, 16, false, true, 2, false, true, 1>, 1, 16);
+    add("TS1 NW4 NTS jt a32", ec_combine<K, 1, 4, false, true, 2, false, true, 2>, 1, 4);
+    add("TS1 NW8 NTS jt a32", ec_combine<K, 1, 8, false, true, 2, false, true, 2>, 1, 8);
+    add("TS1 NW16 NTS jt a32", ec_combine<K, 1, 16, false, true, 2, false, true, 2>, 1, 16);
+    add("TS1 NW16 NTS jt u2", ec_combine<K, 1, 16, false, true, 2, false, true, 1, false, 2>, 1, 16);
+    add("TS1 NW16 NTS jt a32 u2", ec_combine<K, 1, 16, false, true, 2, false, true, 2, false, 2>, 1, 16);
 }
 
 template <int K, int N, typename KF>
@@ -444,7 +445,7 @@ int main(int argc, char **argv)
         };
         addh("heal NW4 NTS", ec_combine<K, 1, 4, false, true>, 4);
         addh("heal NW4 NTS naive", ec_combine<K, 1, 4, false, true, 2, false, false>, 4);
-        addh("heal NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, true>, 4);
+        addh("heal NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 4);
         addh("heal NW8 NTS", ec_combine<K, 1, 8, false, true>, 8);
         addh("heal NW16 NTS", ec_combine<K, 1, 16, false, true>, 16);
         run_group("heal 8+4 (regenerate 4 rows)", v, rounds, iters, s);
@@ -516,8 +517,8 @@ int main(int argc, char **argv)
         };
         addm("mixed TS1 NW4 NTS", ec_combine<K, 1, 4, true, true>, 4);
         addm("mixed TS1 NW8 NTS naive", ec_combine<K, 1, 8, true, true, 2, false, false>, 8);
-        addm("mixed TS1 NW8 NTS jt", ec_combine<K, 1, 8, true, true, 2, false, true, true>, 8);
-        addm("mixed TS1 NW4 NTS jt", ec_combine<K, 1, 4, true, true, 2, false, true, true>, 4);
+        addm("mixed TS1 NW8 NTS jt", ec_combine<K, 1, 8, true, true, 2, false, true, 1>, 8);
+        addm("mixed TS1 NW4 NTS jt", ec_combine<K, 1, 4, true, true, 2, false, true, 1>, 4);
         addm("mixed TS1 NW8 NTS", ec_combine<K, 1, 8, true, true>, 8);
         addm("mixed TS1 NW16 NTS", ec_combine<K, 1, 16, true, true>, 16);
         run_group("decode 8+4 mixed (16 patterns, 1024-stripe groups)", v, rounds, iters, s);
