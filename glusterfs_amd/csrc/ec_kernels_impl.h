@@ -751,9 +751,9 @@ __device__ __forceinline__ uint8_t rmw_byte(const RmwSrc &v, uint64_t o)
 /* W dwords of `p`, which may have any byte alignment.  ROCm runs gfx950 in
  * unaligned access mode, so this is one global_load_dwordx{1,2,4} at the
  * byte address (it touches exactly [p, p + 4W): no over-read into a page
- * the range does not cover).  The earlier form -- W + 1 aligned dword loads
- * funnel-shifted with v_alignbyte_b32 -- ran the 4+2 odd-address partial
- * write at 0.51 of HBM peak (profiles/bench_r01_i.log). */
+ * the range does not cover).  Round 1's realignment issued W + 1 separate
+ * dword loads per plane (0.51 of HBM peak, profiles/bench_r01_i.log); the
+ * one-instruction form below (load_plane_realign) beats both. */
 template <int W>
 __device__ __forceinline__ void load_plane_unaligned(const uint8_t *p, u32 (&d)[W])
 {
@@ -772,6 +772,20 @@ __device__ __forceinline__ void load_plane_unaligned(const uint8_t *p, u32 (&d)[
         d[2] = v.z;
         d[3] = v.w;
     }
+}
+
+/* W dwords starting at `a + sh` bytes, from W + 1 dword-aligned dwords at
+ * `a` funnel-shifted by v_alignbyte_b32 (one global_load_dwordx{2,3,5}).
+ * The extra dword is the one holding the last wanted byte, so the load
+ * never touches a page the wanted range does not. */
+template <int W>
+__device__ __forceinline__ void load_plane_realign(const uint8_t *a, u32 sh, u32 (&d)[W])
+{
+    u32 t[W + 1];
+    __builtin_memcpy(t, __builtin_assume_aligned(a, 4), 4 * (W + 1));
+#pragma unroll
+    for (int i = 0; i < W; ++i)
+        d[i] = __builtin_amdgcn_alignbyte(t[i + 1], t[i], sh);
 }
 
 /* Materialise bytes [o0, o0 + n) of the virtual input into dst (16 bytes
@@ -805,10 +819,14 @@ __global__ __launch_bounds__(kBlock) void ec_rmw_gather(const RmwSrc v, uint64_t
  * stripe 0 and stripe nst-1 (the merged boundary stripes, gathered into
  * `edge` by ec_rmw_gather: edge + 0 and edge + (nedge-1)*stripe) are read
  * aligned; every interior stripe t is read straight from the caller's
- * buffer at user + t*stripe - head with realigned loads, so the interior is
- * never copied (the reference memcpy's the whole write first,
- * ec-inode-write.c:1844). */
-template <int K, int N, int W>
+ * buffer at user + t*stripe - head, so the interior is never copied (the
+ * reference memcpy's the whole write first, ec-inode-write.c:1844).
+ * (Gathering the two boundary stripes inside this kernel instead, byte-wise
+ * through RmwSrc, put the 16+4 instance's inputs in scratch: 316 VGPRs and
+ * 528 B of private memory, 6.9 ms per GiB.)
+ * LM: 0 = byte-address loads (load_plane_unaligned), 1 = dword-aligned loads
+ * funnel-shifted (load_plane_realign); the launcher picks per geometry. */
+template <int K, int N, int W, int LM = 0>
 __global__ __launch_bounds__(kBlock) void ec_encode_vander_rmw(const uint8_t *__restrict__ edge,
                                                                const uint8_t *user_shift,
                                                                const FragPtrs out,
@@ -830,11 +848,22 @@ __global__ __launch_bounds__(kBlock) void ec_encode_vander_rmw(const uint8_t *__
     } else {
         /* user_shift = user - head: the virtual offset of user byte 0 is head */
         const uint8_t *s = user_shift + stripe * S + colb;
+        if constexpr (LM == 0) {
 #pragma unroll
-        for (int j = 0; j < K; ++j)
+            for (int j = 0; j < K; ++j)
 #pragma unroll
-            for (int b = 0; b < 8; ++b)
-                load_plane_unaligned<W>(s + j * ECD_CHUNK + b * 64, x[j][b]);
+                for (int b = 0; b < 8; ++b)
+                    load_plane_unaligned<W>(s + j * ECD_CHUNK + b * 64, x[j][b]);
+        } else {
+            /* every plane of every stripe has the same misalignment */
+            const u32 sh = (u32)(uintptr_t)user_shift & 3u;
+            const uint8_t *al = s - sh;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    load_plane_realign<W>(al + j * ECD_CHUNK + b * 64, sh, x[j][b]);
+        }
     }
     encode_rows<K, W, false, true>(std::make_integer_sequence<int, N>{}, x, out,
                                    stripe * (uint64_t)ECD_CHUNK + colb);

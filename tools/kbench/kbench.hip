@@ -553,5 +553,57 @@ int main(int argc, char **argv)
                              ec_encode_vander<16, 20, 1, true, false>, 1);
         run_group("encode 16+4", v, rounds, iters, s);
     }
+    {   /* partial-stripe write: interior stripes read at an odd address */
+        std::vector<Variant> v;
+        const uint64_t nst = user / (4 * ECD_CHUNK);
+        FragPtrs f;
+        for (int i = 0; i < 6; ++i)
+            f.p[i] = bufB + (uint64_t)i * nst * ECD_CHUNK;
+        const uint8_t *edge = bufA + 2 * user;
+        const uint8_t *ush = bufA + 777;
+        const double bytes = (double)nst * (4 + 6) * ECD_CHUNK;
+        const uint64_t g = (nst * 8 + kBlock - 1) / kBlock;
+        auto addr = [&](const char *nm, auto kern) {
+            v.push_back({nm, bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern, dim3((u32)g), dim3(kBlock), 0, st, edge, ush,
+                                                f, nst);
+                         }, f.p[5], (size_t)nst * ECD_CHUNK});
+        };
+        addr("rmw 4+2 W2 unaligned x2", ec_encode_vander_rmw<4, 6, 2, 0>);
+        addr("rmw 4+2 W2 realign x3", ec_encode_vander_rmw<4, 6, 2, 1>);
+        /* (different input bytes: reported as a MISMATCH, timing only) */
+        add_encode_w<4, 6>(v, "enc 4+2 W2 (aligned input)", nst, bufA, f,
+                           ec_encode_vander<4, 6, 2, false>, 2);
+        run_group("partial write 4+2 (odd address)", v, rounds, iters, s);
+    }
+    {   /* the same for 8+4 and 16+4 (W = 1: one dword per plane per lane) */
+        auto wide = [&](auto kk, auto nn, const char *title, auto k0, auto k1) {
+            constexpr int K = decltype(kk)::value, N = decltype(nn)::value;
+            std::vector<Variant> v;
+            const uint64_t nst = user / (K * ECD_CHUNK);
+            FragPtrs f;
+            for (int i = 0; i < N; ++i)
+                f.p[i] = bufB + (uint64_t)i * nst * ECD_CHUNK;
+            const uint8_t *edge = bufA + 2 * user;
+            const uint8_t *ush = bufA + 777;
+            const double bytes = (double)nst * (K + N) * ECD_CHUNK;
+            const uint64_t g = (nst * 16 + kBlock - 1) / kBlock;
+            auto addr = [&](const char *nm, auto kern) {
+                v.push_back({nm, bytes, [=](hipStream_t st) {
+                                 hipLaunchKernelGGL(kern, dim3((u32)g), dim3(kBlock), 0, st, edge,
+                                                    ush, f, nst);
+                             }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            };
+            addr("rmw W1 unaligned x1", k0);
+            addr("rmw W1 realign x2", k1);
+            run_group(title, v, rounds, iters, s);
+        };
+        wide(std::integral_constant<int, 8>{}, std::integral_constant<int, 12>{},
+             "partial write 8+4 (odd address)", ec_encode_vander_rmw<8, 12, 1, 0>,
+             ec_encode_vander_rmw<8, 12, 1, 1>);
+        wide(std::integral_constant<int, 16>{}, std::integral_constant<int, 20>{},
+             "partial write 16+4 (odd address)", ec_encode_vander_rmw<16, 20, 1, 0>,
+             ec_encode_vander_rmw<16, 20, 1, 1>);
+    }
     return 0;
 }
