@@ -37,6 +37,10 @@
 #include <mutex>
 #include <vector>
 
+#include <cstddef>
+#include <cstring>
+#include <mutex>
+
 #include "ec_kernels.h"
 #include "ec_kernels_impl.h"
 
@@ -125,9 +129,94 @@ int ecdk_has_vander(uint32_t k, uint32_t n)
            (k == 16 && n == 20);
 }
 
+namespace {
+
+/* Device-resident encodes through the tile kernels (LDS-DMA staging of 8
+ * stripes, one row per wave item, NT stores). Same-box kbench A/B against
+ * the register-resident ec_encode_vander (profiles/kbench_r02s.log,
+ * kbench_r02t.log, kbench_r02t_q.log = 0.25 GiB):
+ *   4+2   through ec_combine's jump-table multiply, 16 waves:
+ *         1 GiB 0.494 -> 0.453 ms, 0.25 GiB 0.128 -> 0.111 ms;
+ *   8+4   ec_encode_tile, direct products (no Horner chain), 16 waves:
+ *         1 GiB 0.514 -> 0.459 ms; at 0.25 GiB (64K-stripe batches) the
+ *         register-resident encoder keeps a steadier median (0.126 against
+ *         0.143), so batches up to 128K stripes stay there;
+ *   16+4  ec_encode_tile, Horner, 1 dword per lane, 16 waves:
+ *         1 GiB 0.477 -> 0.446 ms, 0.25 GiB 0.111 -> 0.106 ms. */
+template <int K, int N, int NW, bool DIRECT, int CW>
+int launch_encode_tile(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
+{
+    FragPtrs f;
+    for (int i = 0; i < N; ++i)
+        f.p[i] = static_cast<uint8_t *>(out[i]);
+    const uint64_t g = (nstripes + 7) / 8;
+    if (g == 0)
+        return 0;
+    if (g > 0x7fffffffull)
+        return -EINVAL;
+    hipLaunchKernelGGL((ec_encode_tile<K, N, NW, true, DIRECT, CW>), dim3((u32)g), dim3(NW * 64),
+                       (size_t)K * 8 * ECD_CHUNK, s, static_cast<const uint8_t *>(in), f,
+                       nstripes);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+/* 4+2: the encode matrix (row i: (i+1)^(3-j), ec-method.c:22-36) as one
+ * ec_combine pattern over the stripe-major input */
+int launch_encode_42_combine(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
+{
+    static ecd_combine_desc_t d; /* pattern part built once; pointers per call */
+    static std::once_flag once;
+    std::call_once(once, [] {
+        memset(&d, 0, sizeof(d));
+        d.k = 4;
+        d.rows = 6;
+        d.in_stride = 4 * ECD_CHUNK;
+        d.out_stride = ECD_CHUNK;
+        d.npatterns = 1;
+        d.pat_bytes = 4 + 6 * 4;
+        for (u32 p = 0; p < 4; ++p)
+            d.pat[p] = (uint8_t)p;
+        for (u32 r = 0; r < 6; ++r)
+            for (u32 j = 0; j < 4; ++j)
+                d.pat[4 + r * 4 + j] = (uint8_t)gf_pow_c(r + 1, 3 - (int)j);
+    });
+    ecd_combine_desc_t c;
+    memcpy(&c, &d, offsetof(ecd_combine_desc_t, pat) + 4 + 6 * 4);
+    c.nstripes = nstripes;
+    for (u32 p = 0; p < 4; ++p)
+        c.in_base[p] = static_cast<const uint8_t *>(in) + p * ECD_CHUNK;
+    for (u32 r = 0; r < 6; ++r)
+        c.out_base[r] = out[r];
+    CombineArgs a;
+    const int rc = ecdk_pack_args(&c, &a);
+    if (rc)
+        return rc;
+    return launch_combine<4, 1, 16, 16, true, true, true>(s, a);
+}
+
+} // namespace
+
+/* EC_MI355X_ENC=0 keeps the register-resident encoder for every geometry
+ * (A/B runs only); unset = the shipped choice. */
+static bool enc_tiles()
+{
+    static const bool v = [] {
+        const char *e = getenv("EC_MI355X_ENC");
+        return !(e && *e == '0');
+    }();
+    return v;
+}
+
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                        const void *in, void *const *out, bool zc)
 {
+    const bool tiles = !zc && enc_tiles();
+    if (tiles && k == 4 && n == 6)
+        return launch_encode_42_combine(s, nstripes, in, out);
+    if (tiles && k == 8 && n == 12 && nstripes > (1u << 17))
+        return launch_encode_tile<8, 12, 16, true, 2>(s, nstripes, in, out);
+    if (tiles && k == 16 && n == 20)
+        return launch_encode_tile<16, 20, 16, false, 1>(s, nstripes, in, out);
     if (k == 2 && n == 3)
         return launch_vander<2, 3, 4>(s, nstripes, in, out, zc);
     if (k == 4 && n == 6)

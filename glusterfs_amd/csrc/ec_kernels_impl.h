@@ -205,6 +205,130 @@ __global__ __launch_bounds__(kBlock) void ec_encode_vander(const uint8_t *__rest
                                 stripe * (uint64_t)ECD_CHUNK + colb);
 }
 
+/* Tile encoder: the data of 8 stripes is staged in LDS by LDS-DMA
+ * (global_load_lds_dwordx4, no VGPRs on the read path) into the plane-major
+ * tile of ec_combine -- input chunk p, plane b, stripe s at
+ * ((p * 8 + b) * 8 + s) * 64 -- and every wave then computes whole rows
+ * (fragments) for the 8 stripes by Horner with the row's compile-time
+ * constant v = r + 1 (ec-code-c.c:11647-11657), reading each input chunk
+ * back from LDS.  The row index is wave-uniform, so the dispatch is a
+ * scalar branch to one of N specialised rows.  Where the rows are cheap
+ * (4+2) this beats the register-resident encoder: the LDS-DMA read path
+ * leaves the VGPRs and the vector memory pipe to the stores.
+ * Grid: one block per 8 stripes; LDS = K * 4 KiB. */
+/* GF(2^8) power at compile time (poly 0x11D) */
+constexpr u32 gf_mul_c(u32 a, u32 b)
+{
+    u32 r = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1u)
+            r ^= a;
+        a = ((a << 1) ^ ((a & 0x80u) ? 0x1Du : 0u)) & 0xFFu;
+        b >>= 1;
+    }
+    return r;
+}
+constexpr u32 gf_pow_c(u32 v, int e)
+{
+    return e == 0 ? 1u : gf_mul_c(v, gf_pow_c(v, e - 1));
+}
+
+/* DIRECT = false: Horner, acc = v*acc ^ x_j (a serial chain through acc);
+ * true: acc ^= v^(K-1-j) * x_j, independent products (more ILP, dearer
+ * constants). CW: dwords per plane per lane (2: 8 stripes per wave item,
+ * 1: 4 stripes, two items per row). */
+template <int K, int I, bool NTS, bool DIRECT, int CW>
+__device__ __forceinline__ void encode_tile_row(const uint8_t *col, uint8_t *dst)
+{
+    constexpr u32 T = 8;
+    constexpr u32 v = I + 1;
+    u32 acc[8][CW], y[8][CW];
+    if constexpr (DIRECT && v != 1) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int w = 0; w < CW; ++w)
+                acc[b][w] = 0;
+        static_for<0, K>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const uint8_t *src = col + (u32)j * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+            ecgf::mul_xor<gf_pow_c(v, K - 1 - j), CW, true>(acc, acc, y);
+        });
+    } else {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            load_plane<CW>(col + (u32)b * (T * 64u), acc[b]);
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+            const uint8_t *src = col + (u32)j * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+            if constexpr (v == 1) {
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+#pragma unroll
+                    for (int w = 0; w < CW; ++w)
+                        acc[b][w] ^= y[b][w];
+            } else {
+                ecgf::horner<v, CW, true>(acc, y);
+            }
+        }
+    }
+    store_chunk<CW, NTS>(dst, acc);
+}
+
+template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2>
+__global__ __launch_bounds__(NW * 64) void ec_encode_tile(const uint8_t *__restrict__ in,
+                                                          const FragPtrs out, uint64_t nstripes)
+{
+    constexpr u32 T = 8;
+    constexpr uint64_t S = (uint64_t)K * ECD_CHUNK;
+    constexpr u32 NI = K * T * 32 / 64;      /* LDS-DMA wave instructions per tile */
+    constexpr u32 LPS = 16 / CW, SPI = 64 / LPS, IPR = T / SPI;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+
+    /* stage: instruction ins = planes b, b+1 of input p for the 8 stripes */
+#pragma unroll
+    for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
+        const u32 ins = j * NW + wave;
+        if (ins >= NI)
+            break;
+        const u32 p = ins / (T / 2);
+        const u32 el = (ins * 64 + lane) % (T * 32);
+        const u32 s = (el >> 2) % T;
+        const uint64_t st = t0 + s;
+        if (st < nstripes) {
+            const uint8_t *g = in + st * S + p * ECD_CHUNK + ((el >> 2) / T) * 64u + (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+        }
+    }
+    __syncthreads();
+
+    const u32 cs = lane / LPS, cc = lane % LPS;
+    for (u32 it = wave; it < (u32)N * IPR; it += NW) {
+        const u32 r = __builtin_amdgcn_readfirstlane(it / IPR);
+        const u32 s = (it % IPR) * SPI + cs;
+        const uint64_t ost = t0 + s;
+        const uint8_t *col = lds + s * 64u + cc * (4u * CW);
+        uint8_t *dst = out.p[r] + ost * ECD_CHUNK + cc * (4u * CW);
+        if (ost < nstripes)
+            static_for<0, N>([&](auto I) {
+                if (r == (u32)decltype(I)::value)
+                    encode_tile_row<K, decltype(I)::value, NTS, DIRECT, CW>(col, dst);
+            });
+    }
+}
+
 template <int W>
 inline uint64_t vander_grid(uint64_t nstripes)
 {

@@ -439,9 +439,12 @@ def test_decode_device_8p4_large_batch(ec, oracle, torch_cuda, mask):
 
 
 def test_encode_device_large_batches(ec, oracle, torch_cuda):
-    """Device encode at sizes past one grid wave, every specialised geometry."""
+    """Device encode at sizes past one grid wave, every specialised geometry;
+    8+4 on both sides of the 128K-stripe switch to the tile encoder
+    (ec_kernels.hip ecdk_encode_vander)."""
     torch = torch_cuda
-    for k, n, nst in ((4, 6, 300007), (8, 12, 70001), (16, 20, 20011)):
+    for k, n, nst in ((4, 6, 300007), (8, 12, 70001), (8, 12, (1 << 17) + 3), (16, 20, 20011),
+                      (16, 20, 3)):
         data = rand_bytes(CHUNK * k * nst, seed=nst)
         want = oracle.encode(k, n, data, nthreads=8)
         din = torch.from_numpy(data).cuda()

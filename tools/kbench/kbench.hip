@@ -339,6 +339,70 @@ static void add_encode_w(std::vector<Variant> &vars, const char *nm, uint64_t ns
                     }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
 }
 
+/* GF(2^8) product, poly 0x11D (host side, for building coefficient rows) */
+static uint8_t kb_gmul(uint8_t a, uint8_t b)
+{
+    uint8_t r = 0;
+    while (b) {
+        if (b & 1)
+            r ^= a;
+        a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1D : 0));
+        b >>= 1;
+    }
+    return r;
+}
+
+/* Encode through the generic tile kernel (LDS-DMA staging, NT stores):
+ * rows = n, coefficient (i+1)^(k-1-j) for input j (ec-method.c:22-36). */
+template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2>
+static void add_encode_tile(std::vector<Variant> &vars, const char *nm, uint64_t nst,
+                            const uint8_t *in, const FragPtrs &f)
+{
+    const size_t lds = (size_t)K * 8 * ECD_CHUNK;
+    const uint64_t g = (nst + 7) / 8;
+    vars.push_back({nm, (double)nst * (K + N) * ECD_CHUNK, [=](hipStream_t st) {
+                        hipLaunchKernelGGL((ec_encode_tile<K, N, NW, NTS, DIRECT, CW>), dim3((u32)g),
+                                           dim3(64 * NW), lds, st, in, f, nst);
+                    }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+}
+
+template <int K, int NW, int JT>
+static void add_encode_combine(std::vector<Variant> &vars, const char *nm, int n, uint64_t nst,
+                               const uint8_t *in, const FragPtrs &f)
+{
+    ecd_combine_desc_t d;
+    memset(&d, 0, sizeof(d));
+    d.k = K;
+    d.rows = n;
+    d.nstripes = nst;
+    d.in_stride = (uint64_t)K * ECD_CHUNK;
+    d.out_stride = ECD_CHUNK;
+    for (int p = 0; p < K; ++p) {
+        d.in_base[p] = in + (uint64_t)p * ECD_CHUNK;
+        d.pat[p] = (uint8_t)p;
+    }
+    for (int r = 0; r < n; ++r) {
+        d.out_base[r] = f.p[r];
+        uint8_t v = 1;
+        for (int j = K - 1; j >= 0; --j) {      /* v = (r+1)^(K-1-j) */
+            d.pat[K + r * K + j] = v;
+            v = kb_gmul(v, (uint8_t)(r + 1));
+        }
+    }
+    d.npatterns = 1;
+    d.pat_bytes = K + n * K;
+    CombineArgs *a = new CombineArgs;            /* kept for the process */
+    if (ecdk_pack_args(&d, a))
+        exit(5);
+    const size_t lds = (size_t)K * 8 * ECD_CHUNK;
+    const uint64_t g = (nst + 7) / 8;
+    const CombineArgs *ap = a;
+    vars.push_back({nm, (double)nst * (K + n) * ECD_CHUNK, [=](hipStream_t st) {
+                        hipLaunchKernelGGL((ec_combine<K, 1, NW, false, true, 2, false, true, JT>),
+                                           dim3((u32)g), dim3(64 * NW), lds, st, *ap);
+                    }, f.p[n - 1], (size_t)nst * ECD_CHUNK});
+}
+
 int main(int argc, char **argv)
 {
     const double gib = argc > 1 ? atof(argv[1]) : 1.0;
@@ -536,6 +600,14 @@ int main(int argc, char **argv)
         add_encode_w<4, 6>(v, "enc 4+2 W2", nst, bufA, f, ec_encode_vander<4, 6, 2, false>, 2);
         add_encode_w<4, 6>(v, "enc 4+2 W2 naive", nst, bufA, f,
                            ec_encode_vander<4, 6, 2, false, false>, 2);
+        add_encode_w<4, 6>(v, "enc 4+2 W2 NTS", nst, bufA, f, ec_encode_vander<4, 6, 2, true>, 2);
+        add_encode_combine<4, 8, 1>(v, "enc 4+2 tile NW8 jt", 6, nst, bufA, f);
+        add_encode_combine<4, 16, 1>(v, "enc 4+2 tile NW16 jt", 6, nst, bufA, f);
+        add_encode_tile<4, 6, 16, true>(v, "enc 4+2 vtile NW16 NTS", nst, bufA, f);
+        add_encode_tile<4, 6, 16, true, true>(v, "enc 4+2 vtile NW16 NTS direct", nst, bufA, f);
+        add_encode_tile<4, 6, 16, true, false, 1>(v, "enc 4+2 vtile NW16 NTS CW1", nst, bufA, f);
+        add_encode_tile<4, 6, 16, true, true, 1>(v, "enc 4+2 vtile NW16 NTS direct CW1", nst, bufA, f);
+        add_encode_tile<4, 6, 8, true, true, 1>(v, "enc 4+2 vtile NW8 NTS direct CW1", nst, bufA, f);
         run_group("encode 4+2", v, rounds, iters, s);
         v.clear();
         nst = user / (8 * ECD_CHUNK);
@@ -544,13 +616,37 @@ int main(int argc, char **argv)
         add_encode_w<8, 12>(v, "enc 8+4 W1 NTS naive", nst, bufA, f,
                             ec_encode_vander<8, 12, 1, true, false>, 1);
         add_encode_w<8, 12>(v, "enc 8+4 W2 NTS", nst, bufA, f, ec_encode_vander<8, 12, 2, true>, 2);
+        add_encode_combine<8, 8, 1>(v, "enc 8+4 tile NW8 jt", 12, nst, bufA, f);
+        add_encode_combine<8, 16, 1>(v, "enc 8+4 tile NW16 jt", 12, nst, bufA, f);
+        add_encode_tile<8, 12, 16, true>(v, "enc 8+4 vtile NW16 NTS", nst, bufA, f);
+        add_encode_tile<8, 12, 16, true, true>(v, "enc 8+4 vtile NW16 NTS direct", nst, bufA, f);
+        add_encode_tile<8, 12, 16, true, false, 1>(v, "enc 8+4 vtile NW16 NTS CW1", nst, bufA, f);
+        add_encode_tile<8, 12, 16, true, true, 1>(v, "enc 8+4 vtile NW16 NTS direct CW1", nst, bufA, f);
         run_group("encode 8+4", v, rounds, iters, s);
+        v.clear();
+        {   /* configs[2]: one 64K-stripe batch */
+            const uint64_t n64 = 65536;
+            add_encode_w<8, 12>(v, "enc 8+4 64K W1 NTS", n64, bufA, f,
+                                ec_encode_vander<8, 12, 1, true>, 1);
+            add_encode_combine<8, 16, 1>(v, "enc 8+4 64K tile NW16 jt", 12, n64, bufA, f);
+            add_encode_combine<8, 8, 1>(v, "enc 8+4 64K tile NW8 jt", 12, n64, bufA, f);
+            add_encode_tile<8, 12, 16, true, true, 2>(v, "enc 8+4 64K vtile NW16 NTS direct", n64, bufA, f);
+            add_encode_tile<8, 12, 16, true, true, 1>(v, "enc 8+4 64K vtile NW16 NTS direct CW1", n64, bufA, f);
+            run_group("encode 8+4, 64K stripes", v, rounds, iters, s);
+        }
         v.clear();
         nst = user / (16 * ECD_CHUNK);
         f = frag_ptrs(nst, 20);
         add_encode_w<16, 20>(v, "enc 16+4 W1 NTS", nst, bufA, f, ec_encode_vander<16, 20, 1, true>, 1);
         add_encode_w<16, 20>(v, "enc 16+4 W1 NTS naive", nst, bufA, f,
                              ec_encode_vander<16, 20, 1, true, false>, 1);
+        add_encode_combine<16, 16, 1>(v, "enc 16+4 tile NW16 jt", 20, nst, bufA, f);
+        add_encode_tile<16, 20, 10, true>(v, "enc 16+4 vtile NW10 NTS", nst, bufA, f);
+        add_encode_tile<16, 20, 10, true, true>(v, "enc 16+4 vtile NW10 NTS direct", nst, bufA, f);
+        add_encode_tile<16, 20, 10, true, false, 1>(v, "enc 16+4 vtile NW10 NTS CW1", nst, bufA, f);
+        add_encode_tile<16, 20, 16, true, false, 1>(v, "enc 16+4 vtile NW16 NTS CW1", nst, bufA, f);
+        add_encode_tile<16, 20, 16, true, true, 1>(v, "enc 16+4 vtile NW16 NTS direct CW1", nst, bufA, f);
+        add_encode_tile<16, 20, 16, true, true, 2>(v, "enc 16+4 vtile NW16 NTS direct", nst, bufA, f);
         run_group("encode 16+4", v, rounds, iters, s);
     }
     {   /* partial-stripe write: interior stripes read at an odd address */
