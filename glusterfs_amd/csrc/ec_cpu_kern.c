@@ -147,6 +147,38 @@ void ECC_NAME(ecc_encode)(uint32_t k, uint32_t n, uint64_t nstripes, const uint8
     }
 }
 
+#if defined(__AVX512F__)
+/* One output chunk o = sum_p coef[p] * x_p (zero coefficients skipped) with
+ * the accumulator in registers: the multiply is a switch over the 255
+ * programs inside this function, so the 8 accumulator planes stay in zmm
+ * registers across the inputs (32 zmm hold the accumulator, the input and
+ * the program temporaries), where the mac_tab calls load and store the
+ * accumulator once per input.  AVX-512 only: AVX2 / base would spill. */
+#define ECC_CASE(c)                                                            \
+    case c: {                                                                  \
+        ECGF_PROG_##c                                                          \
+    } break;
+static void combine_row_reg(uint8_t *o, const uint8_t *const *xp, const uint8_t *coef,
+                            uint32_t k)
+{
+    ecc_v a[8] = {{0}};
+    for (uint32_t p = 0; p < k; p++) {
+        const uint8_t c = coef[p];
+        if (c == 0)
+            continue;
+        ecc_v x[8];
+        _Pragma("GCC unroll 8") for (int i = 0; i < 8; i++)
+            x[i] = ld(xp[p] + 64 * i);
+        switch (c) {
+            ECGF_FOR_EACH(ECC_CASE)
+        }
+    }
+    _Pragma("GCC unroll 8") for (int i = 0; i < 8; i++)
+        st(o + 64 * i, a[i]);
+}
+#undef ECC_CASE
+#endif
+
 /* ecd_combine_desc_t semantics (ec_device.h) over stripes [s0, s1); `pats`
  * = the packed patterns {src[k], coef[rows][k]}; zero coefficients are
  * skipped (ec-code-c.c:11666-11676). */
@@ -162,6 +194,15 @@ void ECC_NAME(ecc_combine)(const ecd_combine_desc_t *d, const uint8_t *pats, uin
                 q = d->npatterns - 1; /* clamp, as the kernels do */
         }
         const uint8_t *pat = pats + (size_t)q * d->pat_bytes;
+#if defined(__AVX512F__)
+        const uint8_t *xs[ECD_MAX_ROWS];
+        for (uint32_t p = 0; p < k; p++)
+            xs[p] = (const uint8_t *)d->in_base[pat[p]] + t * d->in_stride;
+        for (uint32_t r = 0; r < d->rows; r++)
+            combine_row_reg((uint8_t *)d->out_base[r] + t * d->out_stride, xs,
+                            pat + k + (size_t)r * k, k);
+        continue;
+#endif
         for (uint32_t r = 0; r < d->rows; r++) {
             uint8_t *o = (uint8_t *)d->out_base[r] + t * d->out_stride;
             const uint8_t *coef = pat + k + (size_t)r * k;

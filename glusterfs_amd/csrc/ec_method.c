@@ -251,12 +251,13 @@ ec_method_inject_device_faults(uint32_t count)
  * library estimates both completion times and takes the shorter:
  *
  *   CPU: user bytes / rate, rate = EC_CPU_ENC_GBPS_K2 (260) / (k + 2) for
- *        encodes and EC_CPU_DEC_GBPS_K (110) / k for decode-type calls
- *        (decode, mixed, heal): 43 / 26 / 14 and 27 / 14 / 7 GB/s per
+ *        encodes and EC_CPU_DEC_GBPS_K (200) / k for decode-type calls
+ *        (decode, mixed, heal): 43 / 26 / 14 and 50 / 25 / 12.5 GB/s per
  *        thread for k = 4 / 8 / 16 with AVX-512 on the MI355X hosts' EPYC
- *        9575F (tools/kbench/xover_cells.sh, profiles/xover_r02i_*.log);
- *        x0.7 with AVX2, x0.4 base x86-64; calls moving more than 32 MiB
- *        (past a CCD's L3) stream from DRAM: min(rate, 22) x 0.9;
+ *        9575F (tools/kbench/xover_cells.sh, profiles/xover_r02k_*.log,
+ *        xover_r02x_dec_*.log); x0.7 with AVX2, x0.4 base x86-64; calls
+ *        moving 32 MiB or more (past a CCD's L3) stream from DRAM:
+ *        min(rate, 24);
  *   GPU: latency + (bytes in flight on the least-loaded host GPU + this
  *        call) / rate, per call: 30 us and 26 GB/s of user data for pinned,
  *        device-mapped buffers (zero copy); 40 us and 14 GB/s for pageable
@@ -292,7 +293,7 @@ xover_init(void)
 {
     ecm_x.cpu_below = env_u64("EC_CPU_BELOW_KB", 0) << 10;
     ecm_x.enc_k2 = env_u64("EC_CPU_ENC_GBPS_K2", 260);
-    ecm_x.dec_k = env_u64("EC_CPU_DEC_GBPS_K", 110);
+    ecm_x.dec_k = env_u64("EC_CPU_DEC_GBPS_K", 200);
     ecm_x.pin_us = env_u64("EC_GPU_PINNED_US", 30);
     ecm_x.pin_gbps = env_u64("EC_GPU_PINNED_GBPS", 26);
     ecm_x.page_us = env_u64("EC_GPU_PAGEABLE_US", 40);
@@ -323,8 +324,8 @@ route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int mappe
     cpu_gbps = (op == ECM_ENCODE ? (double)ecm_x.enc_k2 / (ctx->k + 2)
                                  : (double)ecm_x.dec_k / ctx->k) *
                isa_f[ctx->isa < 0 ? 0 : ctx->isa > 2 ? 2 : ctx->isa];
-    if (moved > (32u << 20))
-        cpu_gbps = (cpu_gbps < 22.0 ? cpu_gbps : 22.0) * 0.9;
+    if (moved >= (32u << 20))
+        cpu_gbps = cpu_gbps < 24.0 ? cpu_gbps : 24.0;
     cpu_us = (double)user / (cpu_gbps * 1e3);
     infl = ecd_host_inflight();
     if (infl == UINT64_MAX)

@@ -9,8 +9,8 @@ mkdir -p gpurun_out
 OUT=gpurun_out/${1:-xover}.log
 SECS=${SECS:-1.0}
 : > "$OUT"
-for k in 4 8 16; do
-  for dec in 0 1; do
+for k in ${KS:-4 8 16}; do
+  for dec in ${OPS:-0 1}; do
     for kib in 128 1024 4096 16384; do
       for thr in 1 16; do
         for mode in gpu cpu auto; do
