@@ -976,17 +976,35 @@ void ecd_inject_faults(uint32_t n)
     g_inject_faults.store(n);
 }
 
+/* Pages already found to be host memory, per thread (direct-mapped).
+ * hipPointerGetAttributes serialises in the HIP runtime -- 0.07 us from one
+ * thread, ~11 us per call with 16 threads on pageable memory
+ * (tools/kbench/ptrq.hip) -- and a host call checks every buffer, so
+ * GlusterFS's recycled iobufs are looked up here first.  Only "host" is
+ * cached: a host virtual address cannot turn into device memory (device
+ * allocations come from the runtime's own reserved range), while device
+ * pointers may be freed and reused by another GPU, so they are queried
+ * every time. */
+static thread_local uintptr_t t_host_page[64];
+
 int ecd_ptr_device(const void *p)
 {
     if (!p || ecd_device_count() == 0)
         return -1;
+    const uintptr_t pg = (uintptr_t)p >> 12;
+    uintptr_t &slot = t_host_page[(pg ^ (pg >> 6) ^ (pg >> 12)) & 63];
+    if (slot == pg + 1)
+        return -1;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
+        slot = pg + 1;
         return -1;
     }
-    if (a.type != hipMemoryTypeDevice)
+    if (a.type != hipMemoryTypeDevice) {
+        slot = pg + 1;
         return -1;
+    }
     for (int i = 0; i < g_ndev; ++i)
         if (g_dev_ids[i] == a.device)
             return i;

@@ -829,7 +829,11 @@ host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
     const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n);
     int rc;
 
-    if (!route_cpu(ctx, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k, bytes, ECM_ENCODE,
+    /* the pinned-buffer GPU estimate is the optimistic one: a call that the
+     * CPU wins against it skips the pointer queries (which serialise in the
+     * HIP runtime: ~11 us each with 16 calling threads, tools/kbench/ptrq) */
+    if (!route_cpu(ctx, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k, bytes, ECM_ENCODE, 1) &&
+        !route_cpu(ctx, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k, bytes, ECM_ENCODE,
                    ecd_host_mapped(in, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k) &&
                        all_mapped((const void *const *)out, ctx->n,
                                   nstripes * EC_METHOD_CHUNK_SIZE))) {
@@ -858,7 +862,8 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
     uint32_t f, r;
     int rc;
 
-    if (!route_cpu(ctx, fl * k, bytes, ECM_DECODE,
+    if (!route_cpu(ctx, fl * k, bytes, ECM_DECODE, 1) &&
+        !route_cpu(ctx, fl * k, bytes, ECM_DECODE,
                    all_mapped(frags, nfrags, fl) &&
                        (outs ? all_mapped((const void *const *)outs, rows, fl)
                              : ecd_host_mapped(out, fl * rows)))) {
