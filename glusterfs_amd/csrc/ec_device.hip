@@ -112,8 +112,20 @@ void host_devices_from_env()
             g_host_devs[g_nhost++] = i;
 }
 
+/* EC_MI355X_DEBUG=1: count the HIP pointer queries of the host-call checks
+ * and print them at exit (development probe for the routing cost). */
+std::atomic<uint64_t> g_ptr_queries{0}, g_map_queries{0};
+
+void print_query_counts()
+{
+    fprintf(stderr, "[ec-mi355x] pointer queries: %llu attribute, %llu mapping\n",
+            (unsigned long long)g_ptr_queries.load(), (unsigned long long)g_map_queries.load());
+}
+
 void discover()
 {
+    if (getenv("EC_MI355X_DEBUG") && atoi(getenv("EC_MI355X_DEBUG")))
+        atexit(print_query_counts);
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess)
         n = 0;
@@ -323,6 +335,7 @@ uint8_t *mapped(const void *p, size_t n)
     if (!p || ((uintptr_t)p & 15))
         return nullptr;
     void *d0 = nullptr, *d1 = nullptr;
+    g_map_queries.fetch_add(1, std::memory_order_relaxed);
     if (hipHostGetDevicePointer(&d0, const_cast<void *>(p), 0) != hipSuccess ||
         (n > 1 && hipHostGetDevicePointer(&d1, (uint8_t *)p + n - 1, 0) != hipSuccess)) {
         (void)hipGetLastError();
@@ -985,17 +998,21 @@ void ecd_inject_faults(uint32_t n)
  * allocations come from the runtime's own reserved range), while device
  * pointers may be freed and reused by another GPU, so they are queried
  * every time. */
-static thread_local uintptr_t t_host_page[64];
+static thread_local uintptr_t t_host_page[256];
 
 int ecd_ptr_device(const void *p)
 {
     if (!p || ecd_device_count() == 0)
         return -1;
     const uintptr_t pg = (uintptr_t)p >> 12;
-    uintptr_t &slot = t_host_page[(pg ^ (pg >> 6) ^ (pg >> 12)) & 63];
+    /* Fibonacci hashing: iobufs sit at regular page strides (65 pages for
+     * 256 KiB mmap'ed buffers), which a xor-fold of the page number mapped
+     * onto a few slots (~4 misses per decode call, 16 threads) */
+    uintptr_t &slot = t_host_page[(uint64_t)(pg * 0x9E3779B97F4A7C15ull) >> 56];
     if (slot == pg + 1)
         return -1;
     hipPointerAttribute_t a;
+    g_ptr_queries.fetch_add(1, std::memory_order_relaxed);
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
         slot = pg + 1;

@@ -220,12 +220,36 @@ typedef struct {
 
 /* ------------------------------------------------------ engine counters */
 
-static uint64_t ecm_stat_gpu, ecm_stat_cpu, ecm_stat_fallback;
+/* Sharded by thread, one cache line per shard: a single shared counter
+ * line written by every call of 16 client threads, next to the read-mostly
+ * crossover constants, cost the CPU path ~2 us per 128 KiB call (false
+ * sharing; tools/kbench/ab_auto_cpu.sh). */
+enum { ECM_STAT_GPU = 0, ECM_STAT_CPU = 1, ECM_STAT_FALLBACK = 2 };
+#define ECM_STAT_SHARDS 64
+static struct {
+    uint64_t c[3];
+} __attribute__((aligned(64))) ecm_stats[ECM_STAT_SHARDS];
+static __thread int ecm_stat_slot = -1;
 
 static void
-stat_add(uint64_t *c)
+stat_add(int which)
 {
-    __atomic_fetch_add(c, 1, __ATOMIC_RELAXED);
+    static unsigned next;
+
+    if (ecm_stat_slot < 0)
+        ecm_stat_slot = (int)(__atomic_fetch_add(&next, 1, __ATOMIC_RELAXED) % ECM_STAT_SHARDS);
+    __atomic_fetch_add(&ecm_stats[ecm_stat_slot].c[which], 1, __ATOMIC_RELAXED);
+}
+
+static uint64_t
+stat_sum(int which)
+{
+    uint64_t v = 0;
+    int i;
+
+    for (i = 0; i < ECM_STAT_SHARDS; i++)
+        v += __atomic_load_n(&ecm_stats[i].c[which], __ATOMIC_RELAXED);
+    return v;
 }
 
 void
@@ -233,9 +257,9 @@ ec_method_get_stats(ec_method_stats_t *st)
 {
     if (!st)
         return;
-    st->gpu_calls = __atomic_load_n(&ecm_stat_gpu, __ATOMIC_RELAXED);
-    st->cpu_calls = __atomic_load_n(&ecm_stat_cpu, __ATOMIC_RELAXED);
-    st->cpu_fallbacks = __atomic_load_n(&ecm_stat_fallback, __ATOMIC_RELAXED);
+    st->gpu_calls = stat_sum(ECM_STAT_GPU);
+    st->cpu_calls = stat_sum(ECM_STAT_CPU);
+    st->cpu_fallbacks = stat_sum(ECM_STAT_FALLBACK);
 }
 
 void
@@ -285,8 +309,8 @@ env_u64(const char *name, uint64_t dflt)
 
 static struct {
     uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, page_gbps_l, always;
-} ecm_x;
-static pthread_once_t ecm_xover_once = PTHREAD_ONCE_INIT;
+} __attribute__((aligned(64))) ecm_x;
+static pthread_once_t ecm_xover_once __attribute__((aligned(64))) = PTHREAD_ONCE_INIT;
 
 static void
 xover_init(void)
@@ -362,7 +386,7 @@ gpu_failed(int rc)
 
     if (rc == 0 || rc == -EINVAL || rc == -E2BIG)
         return 0;
-    stat_add(&ecm_stat_fallback);
+    stat_add(ECM_STAT_FALLBACK);
     if (!__atomic_exchange_n(&logged, 1, __ATOMIC_RELAXED))
         ecm_log("device submission failed (%d: %s); coding on the CPU engine", rc,
                 ecd_last_error());
@@ -840,12 +864,12 @@ host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
         rc = ecd_encode_host(0, ctx->k, ctx->n, nstripes, in, out, ctx->enc_pat);
         if (!gpu_failed(rc)) {
             if (rc == 0)
-                stat_add(&ecm_stat_gpu);
+                stat_add(ECM_STAT_GPU);
             return rc;
         }
     }
     ecc_encode(ctx->isa, ctx->k, ctx->n, nstripes, (const uint8_t *)in, (uint8_t *const *)out);
-    stat_add(&ecm_stat_cpu);
+    stat_add(ECM_STAT_CPU);
     return 0;
 }
 
@@ -871,7 +895,7 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
                              shift);
         if (!gpu_failed(rc)) {
             if (rc == 0)
-                stat_add(&ecm_stat_gpu);
+                stat_add(ECM_STAT_GPU);
             return rc;
         }
     }
@@ -898,7 +922,7 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
     d.group_shift = shift;
     rc = ecc_combine(ctx->isa, &d);
     if (rc == 0)
-        stat_add(&ecm_stat_cpu);
+        stat_add(ECM_STAT_CPU);
     return rc;
 }
 
@@ -1240,13 +1264,13 @@ ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iove
         c = ecd_encode_host_gather(0, ctx->k, ctx->n, nst, ns, segp, segl, out, ctx->enc_pat);
         if (!gpu_failed(c)) {
             if (c == 0)
-                stat_add(&ecm_stat_gpu);
+                stat_add(ECM_STAT_GPU);
             return c;
         }
     }
     c = ecc_encode_gather(ctx->isa, ctx->k, ctx->n, nst, ns, segp, segl, (uint8_t *const *)out);
     if (c == 0)
-        stat_add(&ecm_stat_cpu);
+        stat_add(ECM_STAT_CPU);
     return c;
 }
 

@@ -181,13 +181,20 @@ int main(int argc, char **argv)
     const double secs = argc > 1 ? atof(argv[1]) : 1.0;
     if (argc > 6) { /* one cell: secs k dec reg KiB threads [gen] */
         const uint32_t k = atoi(argv[2]), n = k == 16 ? 20 : k + k / 2;
-        ec_matrix_list_t list;
+        ec_matrix_list_t list, pre;
+        /* SC_PREINIT=1: also bring up the gfx950 engine (HIP) first, to
+         * separate the cost of an initialised HIP runtime from routing */
+        const int preinit = getenv("SC_PREINIT") && atoi(getenv("SC_PREINIT"));
+        if (preinit && ec_method_init(NULL, &pre, k, n, 2 * n, "auto") != 0)
+            return 1;
         if (ec_method_init(NULL, &list, k, n, 2 * n, argc > 7 ? argv[7] : "auto") != 0)
             return 1;
         const size_t sz = ((size_t)atoi(argv[5]) << 10) / (512 * k) * (512 * k);
         const int bad = cell(&list, k, n, ((1u << n) - 1) & ~((1u << (n - k)) - 1), sz,
                              atoi(argv[3]), atoi(argv[4]), atoi(argv[6]), secs);
         ec_method_fini(&list);
+        if (preinit)
+            ec_method_fini(&pre);
         return bad;
     }
     const size_t sizes[] = {128 << 10, 1 << 20, 4 << 20};
