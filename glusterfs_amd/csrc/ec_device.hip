@@ -989,15 +989,17 @@ void ecd_inject_faults(uint32_t n)
     g_inject_faults.store(n);
 }
 
-/* Pages already found to be host memory, per thread (direct-mapped).
+/* Pages already found to be plain host memory, per thread (direct-mapped).
  * hipPointerGetAttributes serialises in the HIP runtime -- 0.07 us from one
  * thread, ~11 us per call with 16 threads on pageable memory
  * (tools/kbench/ptrq.hip) -- and a host call checks every buffer, so
- * GlusterFS's recycled iobufs are looked up here first.  Only "host" is
- * cached: a host virtual address cannot turn into device memory (device
- * allocations come from the runtime's own reserved range), while device
- * pointers may be freed and reused by another GPU, so they are queried
- * every time. */
+ * GlusterFS's recycled iobufs are looked up here first.  Only pages the
+ * runtime does not know at all (pageable malloc / mmap memory: the query
+ * fails) are cached.  Memory the runtime allocated -- device buffers, and
+ * pinned host buffers, which come from the same GPU virtual range -- is
+ * queried every time: once freed, its addresses are handed out again, and a
+ * pinned page cached as "host" came back as a torch device tensor in the GPU
+ * tests (-EINVAL on a device-resident encode). */
 static thread_local uintptr_t t_host_page[256];
 
 int ecd_ptr_device(const void *p)
@@ -1018,10 +1020,8 @@ int ecd_ptr_device(const void *p)
         slot = pg + 1;
         return -1;
     }
-    if (a.type != hipMemoryTypeDevice) {
-        slot = pg + 1;
+    if (a.type != hipMemoryTypeDevice)
         return -1;
-    }
     for (int i = 0; i < g_ndev; ++i)
         if (g_dev_ids[i] == a.device)
             return i;

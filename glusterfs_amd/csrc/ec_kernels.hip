@@ -91,9 +91,10 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
 }
 
 /* NW: waves per block for a single pattern; NWM: for mixed patterns;
- * JTS / JTM: multiply through the jump table (ec_gf8_asm.h) instead of the
- * compiler's switch, for single / mixed patterns */
-template <int K, int TS, int NW, int NWM, bool NTS, bool JTS, bool JTM, bool SL = false>
+ * JTS / JTM: the multiply dispatch for single / mixed patterns (ec_combine's
+ * JT: 0 the compiler's switch, 1 the jump table of ec_gf8_asm.h, 3 the
+ * whole-row asm block of ec_gf8_row.h) */
+template <int K, int TS, int NW, int NWM, bool NTS, int JTS, int JTM, bool SL = false>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     /* sorted slots: every pattern's run may carry up to 7 padding slots */
@@ -191,7 +192,7 @@ int launch_encode_42_combine(hipStream_t s, uint64_t nstripes, const void *in, v
     const int rc = ecdk_pack_args(&c, &a);
     if (rc)
         return rc;
-    return launch_combine<4, 1, 16, 16, true, true, true>(s, a);
+    return launch_combine<4, 1, 16, 16, true, 1, 1>(s, a);
 }
 
 } // namespace
@@ -373,18 +374,20 @@ int launch_combine_slots(hipStream_t s, const CombineArgs &a0)
     }
     if (rc == 0) {
         if (a.k <= 4)
-            rc = launch_combine<4, 1, 8, 8, NTS, true, true, true>(s, a);
+            rc = launch_combine<4, 1, 8, 8, NTS, 1, 1, true>(s, a);
         else if (a.k <= 8)
-            rc = launch_combine<8, 1, 8, 8, NTS, true, true, true>(s, a);
+            rc = launch_combine<8, 1, 8, 8, NTS, 1, 1, true>(s, a);
         else
-            rc = launch_combine<16, 1, 16, 16, NTS, true, true, true>(s, a);
+            rc = launch_combine<16, 1, 16, 16, NTS, 1, 1, true>(s, a);
     }
     (void)hipFreeAsync(ws, s);
     return rc;
 }
 
 /* EC_MI355X_JT=0 / 1 forces the switch / the jump table for every k
- * (tuning A/Bs on one box, tools/ab_jt.sh); unset = the shipped choice. */
+ * (tuning A/Bs on one box, tools/ab_jt.sh); unset = the shipped choice.
+ * (3, the whole-row asm block of ec_gf8_row.h, was A/B'd the same way in
+ * r02z and is not built into the library: profiles/ab_row_r02z.log.) */
 int jt_override()
 {
     static const int v = [] {
@@ -409,8 +412,8 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
      * compiler's switch for A/Bs. */
     const bool sw = jt == 0;
     if (a.k <= 4)
-        return sw ? launch_combine<4, 1, 8, 8, NTS, false, false>(s, a)
-                  : launch_combine<4, 1, 8, 8, NTS, true, true>(s, a);
+        return sw ? launch_combine<4, 1, 8, 8, NTS, 0, 0>(s, a)
+               : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
     if (a.k <= 8) {
         /* Full decodes (rows > 4) of up to 128K stripes use 16-wave blocks:
          * 64K-stripe batches (BASELINE configs[2]) 99.5 -> 91 us for 0xFF0,
@@ -419,13 +422,13 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
          * (profiles/kbench_r01_ts_*.log, ab_r01_nw16.log).  Heal-shaped
          * calls (rows <= 4) keep 4 waves. */
         if (a.rows > 4 && a.nstripes <= (1u << 17))
-            return sw ? launch_combine<8, 1, 16, 8, NTS, false, false>(s, a)
-                      : launch_combine<8, 1, 16, 8, NTS, true, true>(s, a);
-        return sw ? launch_combine<8, 1, 4, 8, NTS, false, false>(s, a)
-                  : launch_combine<8, 1, 4, 8, NTS, true, true>(s, a);
+            return sw ? launch_combine<8, 1, 16, 8, NTS, 0, 0>(s, a)
+                   : launch_combine<8, 1, 16, 8, NTS, 1, 1>(s, a);
+        return sw ? launch_combine<8, 1, 4, 8, NTS, 0, 0>(s, a)
+               : launch_combine<8, 1, 4, 8, NTS, 1, 1>(s, a);
     }
-    return sw ? launch_combine<16, 1, 16, 16, NTS, false, false>(s, a)
-              : launch_combine<16, 1, 16, 16, NTS, true, true>(s, a);
+    return sw ? launch_combine<16, 1, 16, 16, NTS, 0, 0>(s, a)
+           : launch_combine<16, 1, 16, 16, NTS, 1, 1>(s, a);
 }
 
 /* pack, then launch; -E2BIG from the packer means "use a device table" */

@@ -625,6 +625,16 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
         const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
         u32 acc[8][CW], y[8][CW];
+        if constexpr (JT == 3) {
+            /* the whole row in one asm block (ec_gf8_row.h) */
+            static_assert(CW == 2 && T == 8, "row asm: 8-stripe tiles, 2 dwords per lane");
+            const u32 va = (u32)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)col;
+            ecgf::row_jt<K>(acc, va, w0, w1, w2, w3, k);
+            const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
+            if (ost != kNoSlot)
+                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
+            continue;
+        }
 #pragma unroll
         for (int b = 0; b < 8; ++b)
 #pragma unroll

@@ -312,20 +312,15 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
      * r02: the searched multiply programs of ec_gf8_prog.h ("CSE", the
      * default) against the round-1 per-plane trees ("naive"); the bit-pair
      * candidate kb_combine_bp lost in r01 and is no longer timed) */
-    add("TS1 NW4 NTS", ec_combine<K, 1, 4, false, true>, 1, 4);
-    add("TS1 NW4 NTS naive", ec_combine<K, 1, 4, false, true, 2, false, false>, 1, 4);
-    add("TS1 NW8 NTS", ec_combine<K, 1, 8, false, true>, 1, 8);
-    add("TS1 NW8 NTS naive", ec_combine<K, 1, 8, false, true, 2, false, false>, 1, 8);
-    add("TS1 NW16 NTS", ec_combine<K, 1, 16, false, true>, 1, 16);
-    add("TS1 NW16 NTS naive", ec_combine<K, 1, 16, false, true, 2, false, false>, 1, 16);
+    /* r02 (kbench_r02t.log and earlier): switch / naive / aligned / unrolled
+     * variants retired; the shipped jump table (jt) against the whole-row
+     * asm block of ec_gf8_row.h (row) */
     add("TS1 NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 1, 4);
     add("TS1 NW8 NTS jt", ec_combine<K, 1, 8, false, true, 2, false, true, 1>, 1, 8);
     add("TS1 NW16 NTS jt", ec_combine<K, 1, 16, false, true, 2, false, true, 1>, 1, 16);
-    add("TS1 NW4 NTS jt a32", ec_combine<K, 1, 4, false, true, 2, false, true, 2>, 1, 4);
-    add("TS1 NW8 NTS jt a32", ec_combine<K, 1, 8, false, true, 2, false, true, 2>, 1, 8);
-    add("TS1 NW16 NTS jt a32", ec_combine<K, 1, 16, false, true, 2, false, true, 2>, 1, 16);
-    add("TS1 NW16 NTS jt u2", ec_combine<K, 1, 16, false, true, 2, false, true, 1, false, 2>, 1, 16);
-    add("TS1 NW16 NTS jt a32 u2", ec_combine<K, 1, 16, false, true, 2, false, true, 2, false, 2>, 1, 16);
+    add("TS1 NW4 NTS row", ec_combine<K, 1, 4, false, true, 2, false, true, 3>, 1, 4);
+    add("TS1 NW8 NTS row", ec_combine<K, 1, 8, false, true, 2, false, true, 3>, 1, 8);
+    add("TS1 NW16 NTS row", ec_combine<K, 1, 16, false, true, 2, false, true, 3>, 1, 16);
 }
 
 template <int K, int N, typename KF>
@@ -512,6 +507,8 @@ int main(int argc, char **argv)
         addh("heal NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 4);
         addh("heal NW8 NTS", ec_combine<K, 1, 8, false, true>, 8);
         addh("heal NW16 NTS", ec_combine<K, 1, 16, false, true>, 16);
+        addh("heal NW4 NTS row", ec_combine<K, 1, 4, false, true, 2, false, true, 3>, 4);
+        addh("heal NW8 NTS row", ec_combine<K, 1, 8, false, true, 2, false, true, 3>, 8);
         run_group("heal 8+4 (regenerate 4 rows)", v, rounds, iters, s);
     }
     {   /* 16+4 decode, dense */
@@ -585,6 +582,8 @@ int main(int argc, char **argv)
         addm("mixed TS1 NW4 NTS jt", ec_combine<K, 1, 4, true, true, 2, false, true, 1>, 4);
         addm("mixed TS1 NW8 NTS", ec_combine<K, 1, 8, true, true>, 8);
         addm("mixed TS1 NW16 NTS", ec_combine<K, 1, 16, true, true>, 16);
+        addm("mixed TS1 NW8 NTS row", ec_combine<K, 1, 8, true, true, 2, false, true, 3>, 8);
+        addm("mixed TS1 NW4 NTS row", ec_combine<K, 1, 4, true, true, 2, false, true, 3>, 4);
         run_group("decode 8+4 mixed (16 patterns, 1024-stripe groups)", v, rounds, iters, s);
     }
     if (!getenv("KB_NO_ENCODE")) {   /* encode 4+2, 8+4, 16+4: shipped W/NTS, CSE vs naive */
@@ -649,7 +648,7 @@ int main(int argc, char **argv)
         add_encode_tile<16, 20, 16, true, true, 2>(v, "enc 16+4 vtile NW16 NTS direct", nst, bufA, f);
         run_group("encode 16+4", v, rounds, iters, s);
     }
-    {   /* partial-stripe write: interior stripes read at an odd address */
+    if (!getenv("KB_NO_RMW")) {   /* partial-stripe write: interior stripes read at an odd address */
         std::vector<Variant> v;
         const uint64_t nst = user / (4 * ECD_CHUNK);
         FragPtrs f;
@@ -672,7 +671,7 @@ int main(int argc, char **argv)
                            ec_encode_vander<4, 6, 2, false>, 2);
         run_group("partial write 4+2 (odd address)", v, rounds, iters, s);
     }
-    {   /* the same for 8+4 and 16+4 (W = 1: one dword per plane per lane) */
+    if (!getenv("KB_NO_RMW")) {   /* the same for 8+4 and 16+4 (W = 1: one dword per plane per lane) */
         auto wide = [&](auto kk, auto nn, const char *title, auto k0, auto k1) {
             constexpr int K = decltype(kk)::value, N = decltype(nn)::value;
             std::vector<Variant> v;
