@@ -44,6 +44,7 @@ sys.path.insert(0, ROOT)
 METRIC = "EC encode/decode user-data GB/s (4+2, 8+4) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 CHUNK = 512
+EXTRA_WARMUP = 20  # untimed launches before each `extra` config (extra_configs)
 
 
 def parse():
@@ -317,9 +318,16 @@ def frac(nbytes, seconds):
 
 
 def extra_configs(c, steps, warmup):
+    """BASELINE's other configs, each timed like the headline over max(3,
+    steps/2) launches -- after at least EXTRA_WARMUP untimed ones: a 60-launch
+    kernel trace (profiles/sustain_r02l.log) shows the 16+4 decode at ~400 us,
+    rising to ~515 us around launches 6-12 and settling back to 390-410 us,
+    so a short warm-up times that clock transient instead of the kernel."""
     torch = c.torch
     st = max(3, steps // 2)
-    ex = {"copy_calibration_GBps": copy_calibration(torch, c.dev, st)}
+    warmup = max(warmup, EXTRA_WARMUP)
+    ex = {"copy_calibration_GBps": copy_calibration(torch, c.dev, st),
+          "timing": "%d launches after %d warm-up launches per config" % (st, warmup)}
 
     def put(name, r, alg):
         ex[name] = dict(user_GBps=round(gbps(r["user"], r["kernel_s"]), 1),
@@ -369,8 +377,9 @@ def dist_configs(c, grp, steps, warmup):
     steps / max-over-ranks wall time between barriers."""
     torch = c.torch
     st = max(3, steps // 2)
+    warmup = max(warmup, EXTRA_WARMUP)          # as in extra_configs
     W = grp.world
-    ex = {}
+    ex = {"timing": "%d launches after %d warm-up launches per config" % (st, warmup)}
 
     def put(name, r, alg_per_user):
         wall = grp.max(r["wall"])

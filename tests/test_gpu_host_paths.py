@@ -205,3 +205,41 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def _attr_queries(kind):
+    """HIP pointer-attribute queries made by 4 host encodes of 8 stripes on
+    `kind` buffers (EC_MI355X_DEBUG=1 prints the count at exit)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import numpy as np, glusterfs_amd as g\n"
+        "L = g.ECMatrixList(4, 6)\n"
+        "if %r == 'pinned':\n"
+        "    bufs = [g.PinnedArray(512 * 4 * 8)] + [g.PinnedArray(512 * 8) for _ in range(6)]\n"
+        "    arrs = [b.array for b in bufs]\n"
+        "else:\n"
+        "    arrs = [np.zeros(512 * 4 * 8, np.uint8)] + [np.zeros(512 * 8, np.uint8) for _ in range(6)]\n"
+        "for _ in range(4):\n"
+        "    L.encode_batch(8, arrs[0], arrs[1:])\n" % kind)
+    env = dict(os.environ, EC_MI355X_DEBUG="1", EC_MI355X_QUIET="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stderr.splitlines() if "pointer queries" in l][-1]
+    return int(line.split("queries:")[1].split()[0])
+
+
+def test_pinned_pages_are_queried_every_call(ec):
+    """The per-thread host-page cache (ec_device.hip ecd_ptr_device) keeps
+    only pages the HIP runtime does not know.  Pinned host pages come from
+    the runtime's GPU virtual range: freed, their addresses are handed out
+    again, also for device buffers -- a cached "host" verdict then routed a
+    device-resident call as a host one (-EINVAL, r02z).  So pinned buffers
+    are queried on every call, pageable ones once."""
+    pinned = _attr_queries("pinned")
+    pageable = _attr_queries("pageable")
+    assert pinned >= 4 * 7, pinned          # every buffer, every call
+    assert pageable <= 7 + 2, pageable      # first call only

@@ -271,6 +271,125 @@ __global__ __launch_bounds__(NW * 64) void kb_combine_bp(const CombineArgs a)
     }
 }
 
+/* Candidate (r02z): persistent blocks with a double-buffered LDS tile.
+ * ec_combine stages a tile, waits, computes and stores, so a CU's memory
+ * pipe idles whenever its resident blocks all compute at once; at k = 16
+ * only two 64 KiB tiles fit a CU.  Here one block per CU loops over tiles
+ * t, t + grid, ...: the LDS-DMA loads of tile t+2G are issued into the
+ * buffer tile t has just released, so every compute phase runs with the
+ * next tile's loads (and this tile's stores) in flight.  The wait for tile
+ * t's loads counts only what this wave issued after them (the stores of the
+ * previous tile and the loads of the next): vector memory operations
+ * complete in issue order on gfx9, so vmcnt(N) with N <= that count means
+ * tile t has landed. */
+__device__ __forceinline__ void kb_wait_vm_atmost(u32 n)
+{
+    /* s_waitcnt takes an immediate: pick the largest encodable bound <= n */
+#define KB_VM(N) (((N) & 15) | (((N) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+    if (n >= 24)
+        __builtin_amdgcn_s_waitcnt(KB_VM(24));
+    else if (n >= 16)
+        __builtin_amdgcn_s_waitcnt(KB_VM(16));
+    else if (n >= 12)
+        __builtin_amdgcn_s_waitcnt(KB_VM(12));
+    else if (n >= 8)
+        __builtin_amdgcn_s_waitcnt(KB_VM(8));
+    else if (n >= 4)
+        __builtin_amdgcn_s_waitcnt(KB_VM(4));
+    else if (n >= 2)
+        __builtin_amdgcn_s_waitcnt(KB_VM(2));
+    else
+        __builtin_amdgcn_s_waitcnt(KB_VM(0));
+#undef KB_VM
+}
+
+template <int K, int NW, bool NTS>
+__global__ __launch_bounds__(NW * 64) void kb_combine_db(const CombineArgs a)
+{
+    constexpr u32 T = 8;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const u32 tile_bytes = k * T * ECD_CHUNK;
+    const uint64_t ntiles = (a.nstripes + T - 1) / T;
+    const u32 ni = k * (T / 2);                       /* wave instructions per tile */
+    const PatWords<false> pw(a, 0u, lane, nullptr);
+    /* stage tile `tl` into buffer `bf`; returns this wave's instruction count */
+    auto stage = [&](uint64_t tl, u32 bf) -> u32 {
+        u32 n = 0;
+        for (u32 ins = wave; ins < ni; ins += NW) {
+            const u32 p = ins / (T / 2);
+            const u32 el = (ins * 64 + lane) % (T * 32);
+            const u32 s = (el >> 2) % T;
+            const uint64_t st = tl * T + s;
+            /* past the data: re-read the last stripe (keeps the count uniform) */
+            const uint64_t sc = st < a.nstripes ? st : a.nstripes - 1;
+            const uint8_t *g = a.in_base[pw.byte(a, p)] + sc * a.in_stride +
+                               ((el >> 2) / T) * 64u + (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + bf * tile_bytes + ins * 1024u),
+                16, 0, 0);
+            ++n;
+        }
+        return n;
+    };
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles)
+        return;
+    u32 after = 0;                                  /* ops issued after tile t's loads */
+    stage(t, 0);
+    if (t + gridDim.x < ntiles)
+        after = stage(t + gridDim.x, 1);
+    const u32 cs = lane >> 3, cc = lane & 7u;
+    const u32 items = a.rows;
+    for (u32 bf = 0; t < ntiles; t += gridDim.x, bf ^= 1u) {
+        kb_wait_vm_atmost(after);
+        __syncthreads();
+        const uint8_t *base = lds + bf * tile_bytes;
+        u32 nst = 0;
+        for (u32 r = wave; r < items; r += NW) {
+            const uint8_t *col = base + cs * 64u + cc * 8u;
+            const u32 rw = a.kw * (1 + r);
+            const u32 w0 = pw.word(a, rw);
+            const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+            const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
+            const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
+            u32 acc[8][2], y[8][2];
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                acc[b][0] = acc[b][1] = 0;
+            uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+            uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
+#pragma unroll 1
+            for (u32 p = 0; p < k; ++p) {
+                const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+                cl = (cl >> 8) | (ch << 56);
+                ch >>= 8;
+                if (c == 0)
+                    continue;
+                const uint8_t *src = col + p * (T * ECD_CHUNK);
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    load_plane<2>(src + (u32)b * (T * 64u), y[b]);
+                ecgf::mul_xor_jt<2>(c, acc, y);
+            }
+            const uint64_t ost = t * T + cs;
+            if (ost < a.nstripes)
+                store_chunk<2, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+            nst += 8;                                /* stores counted per wave */
+        }
+        __syncthreads();                             /* buffer bf is free */
+        u32 nl = 0;
+        if (t + 2ull * gridDim.x < ntiles)
+            nl = stage(t + 2ull * gridDim.x, bf);
+        /* next iteration waits for tile t+G, issued before these stores and loads */
+        after = nst + nl;
+    }
+}
+
 /* decode k+r with the first r bricks missing, coefficients from the host
  * inverse (a dense k x k matrix is all we need for timing; correctness of
  * the math is covered by the parity tests -- here variants are compared
@@ -321,6 +440,30 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     add("TS1 NW4 NTS row", ec_combine<K, 1, 4, false, true, 2, false, true, 3>, 1, 4);
     add("TS1 NW8 NTS row", ec_combine<K, 1, 8, false, true, 2, false, true, 3>, 1, 8);
     add("TS1 NW16 NTS row", ec_combine<K, 1, 16, false, true, 2, false, true, 3>, 1, 16);
+    /* persistent double-buffered tiles: `bpc` blocks per CU */
+    auto adddb = [&](const char *nm, auto kern, int nw, int bpc) {
+        const size_t lds = 2 * (size_t)K * 8 * ECD_CHUNK;
+        CHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+        const uint64_t tiles = (nst + 7) / 8;
+        const uint64_t g = std::min<uint64_t>(tiles, 256ull * bpc);
+        vars.push_back({nm, bytes, [=](hipStream_t s) {
+                            hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * nw), lds, s, a);
+                        }, out, ob});
+    };
+    if (K == 16) {
+        adddb("db NW16 x1", kb_combine_db<K, 16, true>, 16, 1);
+        adddb("db NW8 x1", kb_combine_db<K, 8, true>, 8, 1);
+        adddb("db NW16 x2", kb_combine_db<K, 16, true>, 16, 2);
+    } else if (K == 8) {
+        adddb("db NW16 x1", kb_combine_db<K, 16, true>, 16, 1);
+        adddb("db NW8 x2", kb_combine_db<K, 8, true>, 8, 2);
+        adddb("db NW16 x2", kb_combine_db<K, 16, true>, 16, 2);
+    } else {
+        adddb("db NW8 x2", kb_combine_db<K, 8, true>, 8, 2);
+        adddb("db NW8 x4", kb_combine_db<K, 8, true>, 8, 4);
+        adddb("db NW16 x2", kb_combine_db<K, 16, true>, 16, 2);
+    }
 }
 
 template <int K, int N, typename KF>
