@@ -422,12 +422,14 @@ def test_decode_device_every_mask(ec, oracle, torch_cuda, k, n, nst):
     _device_decode_masks(ec, oracle, torch_cuda, k, n, masks, nst, seed=k * 31 + n)
 
 
-def test_decode_device_sampled_masks_16p4(ec, oracle, torch_cuda):
-    """200 sampled masks of 16+4 on the device-resident path (k = 16 kernel)."""
+def test_decode_device_every_mask_16p4(ec, oracle, torch_cuda):
+    """Every one of the 4845 masks of 16+4 on the device-resident path (the
+    k = 16 kernel bench.py times), 13 stripes: one full 8-stripe tile and a
+    ragged one."""
     k, n = 16, 20
     allm = [sum(1 << b for b in c) for c in itertools.combinations(range(n), k)]
-    pick = np.random.default_rng(16).choice(len(allm), 200, replace=False)
-    _device_decode_masks(ec, oracle, torch_cuda, k, n, [allm[i] for i in pick], 45, seed=1604)
+    assert len(allm) == 4845
+    _device_decode_masks(ec, oracle, torch_cuda, k, n, allm, 13, seed=1604)
 
 
 @pytest.mark.parametrize("mask", [0xFF0, 0xEB5])
