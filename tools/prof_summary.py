@@ -19,7 +19,7 @@ import json
 import os
 import sys
 
-OURS = ("ec_combine", "ec_encode_vander")
+OURS = ("ec_combine", "ec_encode_vander", "ec_encode_tile", "ec_slots")
 
 
 def short(name):
@@ -64,9 +64,10 @@ def algorithmic(cfg, gib):
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     traffic_path = sys.argv[3] if len(sys.argv) > 3 else None
+    # GiB per config as tools/gpu_final.sh passes them
     gib = {"dec_4p2_3C": 1, "enc_4p2": 1, "enc_8p4": 0.25, "dec_8p4_FF0": 0.25,
            "enc_16p4": 2, "dec_8p4_EB5": 0.25, "dec_4p2_0F": 1, "mixed_8p4": 1, "heal_8p4": 1,
-           "dec_16p4_FFFF0": 1}
+           "dec_16p4_FFFF0": 1, "mixed_16p4_64": 1, "rmw_4p2": 1}
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     lines = ["# rocprofv3 summary (%s)" % os.path.basename(src.rstrip("/")), "",
              "| config | kernel | calls | avg us | user GB/s | algorithmic GB/s | HBM frac "
@@ -84,6 +85,10 @@ def main():
         # encode configs also run one decode for the parity check
         if cfg.startswith("enc"):
             kern = next((k for k in st if "encode" in k), kern)
+        elif cfg.startswith("mixed") and any(k.startswith("ec_slots") for k in st):
+            # sorted-slot groups: the tile kernel after the sort kernels
+            kern = max((k for k in st if k.startswith("ec_combine")),
+                       key=lambda k: st[k]["calls"] * st[k]["avg_ns"])
         elif any(k.startswith("ec_combine") for k in st):
             # the timed combine launches dominate the one setup encode
             kern = max((k for k in st if k.startswith("ec_combine")),

@@ -17,7 +17,7 @@ while [ $# -ge 2 ]; do
     if [ $PASS = trace ]; then ARGS="--kernel-trace --stats"; else ARGS="--kernel-trace --kernel-include-regex ec_ --pmc $PASS"; fi
     echo "[$(date +%T)] $CFG $PASS"
     timeout -k 10 300 rocprofv3 $ARGS -d "$OUT/${NAME}_$PASS" -o run --output-format csv -- \
-      python3 "$R/bench.py" --only "$CFG" --gib "$GIB" --steps 10 --warmup 2 \
+      python3 "$R/bench.py" --only "$CFG" --gib "$GIB" --steps 40 --warmup 10 \
       > "$OUT/${NAME}_$PASS.log" 2>&1
     rc=$?
     echo "rc=$rc"; tail -2 "$OUT/${NAME}_$PASS.log"
