@@ -995,9 +995,9 @@ void ecd_inject_faults(uint32_t n)
  * (tools/kbench/ptrq.hip) -- and a host call checks every buffer, so
  * GlusterFS's recycled iobufs are looked up here first.  Only pages the
  * runtime does not know at all (pageable malloc / mmap memory: the query
- * fails) are cached.  Memory the runtime allocated -- device buffers, and
- * pinned host buffers, which come from the same GPU virtual range -- is
- * queried every time: once freed, its addresses are handed out again, and a
+ * reports hipMemoryTypeUnregistered, or fails) are cached.  Memory the
+ * runtime allocated -- device buffers, and pinned host buffers, which come
+ * from the same GPU virtual range -- is queried every time: once freed, its addresses are handed out again, and a
  * pinned page cached as "host" came back as a torch device tensor in the GPU
  * tests (-EINVAL on a device-resident encode). */
 static thread_local uintptr_t t_host_page[256];
@@ -1020,8 +1020,11 @@ int ecd_ptr_device(const void *p)
         slot = pg + 1;
         return -1;
     }
-    if (a.type != hipMemoryTypeDevice)
+    if (a.type != hipMemoryTypeDevice) {
+        if (a.type == hipMemoryTypeUnregistered)
+            slot = pg + 1;
         return -1;
+    }
     for (int i = 0; i < g_ndev; ++i)
         if (g_dev_ids[i] == a.device)
             return i;

@@ -85,6 +85,8 @@ def main():
         # encode configs also run one decode for the parity check
         if cfg.startswith("enc"):
             kern = next((k for k in st if "encode" in k), kern)
+        elif cfg.startswith("rmw"):
+            kern = next((k for k in st if "rmw" in k and "gather" not in k), kern)
         elif cfg.startswith("mixed") and any(k.startswith("ec_slots") for k in st):
             # sorted-slot groups: the tile kernel after the sort kernels
             kern = max((k for k in st if k.startswith("ec_combine")),
