@@ -20,7 +20,6 @@
 
 #include "ec_gf8_asm.h"
 #include "ec_gf8_prog.h"
-#include "ec_gf8_row.h"
 
 namespace ecgf {
 
@@ -200,22 +199,6 @@ __device__ __forceinline__ void mul_xor_jt(u32 c, u32 (&acc)[8][W], const u32 (&
         ECGF_ASM_DISPATCH_W2_A32(acc, x, t, c);  /* bodies on 32-byte boundaries */
     else
         ECGF_ASM_DISPATCH_W2(acc, x, t, c);
-}
-
-/* acc = XOR_{p<k} c_p * x_p for one ec_combine row: c_p is byte p % 4 of
- * word p / 4 of (w0..w3), x_p input p of the tile at LDS byte address va
- * (8-stripe plane-major tile, plane b at va + (p*8 + b) * 512); k <= K. */
-template <int K>
-__device__ __forceinline__ void row_jt(u32 (&acc)[8][2], u32 va, u32 w0, u32 w1, u32 w2,
-                                       u32 w3, u32 k)
-{
-    static_assert(K == 4 || K == 8 || K == 16, "row asm is generated for K = 4, 8, 16");
-    if constexpr (K == 4)
-        ECGF_ASM_ROW_K4(acc, va, w0, w1, w2, w3, k);
-    else if constexpr (K == 8)
-        ECGF_ASM_ROW_K8(acc, va, w0, w1, w2, w3, k);
-    else
-        ECGF_ASM_ROW_K16(acc, va, w0, w1, w2, w3, k);
 }
 
 } // namespace ecgf

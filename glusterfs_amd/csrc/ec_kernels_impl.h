@@ -556,34 +556,14 @@ __device__ __forceinline__ uint64_t slot_stripe(const CombineArgs &a, uint64_t s
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
 /* JT: 0 = the compiler's switch, 1 = the jump table of ec_gf8_asm.h, 2 = the
- * same with 32-byte-aligned bodies.
+ * same with 32-byte-aligned bodies.  (r02z also A/B'd a whole-row asm block
+ * and grouped waits on the staged inputs; neither was faster: DESIGN.md 3.4,
+ * code in commit 87d127c.)
  * SLOTS: mixed patterns with groups below a tile (1, 2, 4 stripes): the
  * stripes were sorted by pattern into 8-slot tiles (ec_slots_* kernels), and
  * the block reads its tile's stripes from the slot list. */
-/* SPLIT (r02z candidate): wait for the staged inputs group by group -- the
- * inputs wave instruction j of every wave brings in -- so the first inputs'
- * products run while the later ones are still landing, instead of one
- * wait for the whole tile.  Needs at most one (row, subtile) item per wave,
- * since every wave must pass the same barriers. */
-__device__ __forceinline__ void wait_vm_atmost(u32 n)
-{
-    /* s_waitcnt vmcnt(n) (gfx9 encoding; expcnt / lgkmcnt left at maximum) */
-#define ECK_VM(N) (((N) & 15) | (((N) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
-    switch (n) {
-    case 0: __builtin_amdgcn_s_waitcnt(ECK_VM(0)); break;
-    case 1: __builtin_amdgcn_s_waitcnt(ECK_VM(1)); break;
-    case 2: __builtin_amdgcn_s_waitcnt(ECK_VM(2)); break;
-    case 3: __builtin_amdgcn_s_waitcnt(ECK_VM(3)); break;
-    case 4: __builtin_amdgcn_s_waitcnt(ECK_VM(4)); break;
-    case 5: __builtin_amdgcn_s_waitcnt(ECK_VM(5)); break;
-    case 6: __builtin_amdgcn_s_waitcnt(ECK_VM(6)); break;
-    default: __builtin_amdgcn_s_waitcnt(ECK_VM(7)); break;
-    }
-#undef ECK_VM
-}
-
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1, bool SPLIT = false>
+          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -632,82 +612,11 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                 (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
         }
     }
-    const u32 cs = lane / LPS, cc = lane % LPS;
-    const u32 items = a.rows * IPT;
-    if constexpr (SPLIT && !PG && JT == 1 && CW == 2 && T == 8 && NW >= 4) {
-        /* group j = the inputs of every wave's j-th staging instruction:
-         * p in [j * NW/4, (j+1) * NW/4) */
-        constexpr u32 PG_ = NW / 4;
-        constexpr u32 JMAX = (NI + NW - 1) / NW;
-        static_assert(JMAX <= 8, "wait_vm_atmost covers 8 groups");
-        if (items <= NW) {
-            const u32 ng = (k + PG_ - 1) / PG_;
-            /* this wave's staging instructions (the loop above) */
-            u32 mine = 0;
-            for (u32 j = 0; j < JMAX; ++j)
-                mine += (j * NW + wave < NI && (j * NW + wave) / (T / 2) < k) ? 1u : 0u;
-            const bool has = wave < items;
-            const u32 r = has ? wave / IPT : 0u, s = (wave % IPT) * SPI + cs;
-            const uint8_t *col = lds + s * 64u + cc * 8u;
-            const u32 rw = a.kw * (1 + r);
-            const u32 w0 = pw.word(a, rw);
-            const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
-            const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
-            const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
-            u32 acc[8][2], y[8][2];
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-                acc[b][0] = acc[b][1] = 0;
-            uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
-            uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
-            u32 p = 0;
-#pragma unroll 1
-            for (u32 g = 0; g < ng; ++g) {
-                wait_vm_atmost(mine > g + 1 ? mine - g - 1 : 0u);
-                asm volatile("" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                if (!has)
-                    continue;
-                const u32 pe = min(k, (g + 1) * PG_);
-#pragma unroll 1
-                for (; p < pe; ++p) {
-                    const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
-                    cl = (cl >> 8) | (ch << 56);
-                    ch >>= 8;
-                    if (c == 0)                  /* ec-code-c.c:11666-11676 */
-                        continue;
-                    /* the 8 planes by LDS reads in asm: the compiler
-                     * would put a vmcnt(0) before a plain LDS read behind
-                     * pending LDS-DMA (it cannot tell which group landed) */
-                    const u32 va = (u32)(uintptr_t)(const __attribute__((address_space(3)))
-                                                        uint8_t *)(col + p * (T * ECD_CHUNK));
-                    v4u q0, q1, q2, q3;
-                    asm volatile("ds_read2st64_b64 %0, %4 offset1:1\n"
-                                 "ds_read2st64_b64 %1, %4 offset0:2 offset1:3\n"
-                                 "ds_read2st64_b64 %2, %4 offset0:4 offset1:5\n"
-                                 "ds_read2st64_b64 %3, %4 offset0:6 offset1:7\n"
-                                 "s_waitcnt lgkmcnt(0)"
-                                 : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3)
-                                 : "v"(va));
-                    y[0][0] = q0[0]; y[0][1] = q0[1]; y[1][0] = q0[2]; y[1][1] = q0[3];
-                    y[2][0] = q1[0]; y[2][1] = q1[1]; y[3][0] = q1[2]; y[3][1] = q1[3];
-                    y[4][0] = q2[0]; y[4][1] = q2[1]; y[5][0] = q2[2]; y[5][1] = q2[3];
-                    y[6][0] = q3[0]; y[6][1] = q3[1]; y[7][0] = q3[2]; y[7][1] = q3[3];
-                    ecgf::mul_xor_jt<2>(c, acc, y);
-                }
-            }
-            if (has) {
-                const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
-                if (ost != kNoSlot)
-                    store_chunk<2, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
-            }
-            return;
-        }
-    }
     __syncthreads();
 
     /* compute: (row, 8-stripe subtile) items spread over the NW waves */
+    const u32 cs = lane / LPS, cc = lane % LPS;
+    const u32 items = a.rows * IPT;
     for (u32 it = wave; it < items; it += NW) {
         const u32 r = it / IPT, s = (it % IPT) * SPI + cs;
         const uint8_t *col = lds + s * 64u + cc * (4u * CW);
@@ -718,16 +627,6 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
         const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
         u32 acc[8][CW], y[8][CW];
-        if constexpr (JT == 3) {
-            /* the whole row in one asm block (ec_gf8_row.h) */
-            static_assert(CW == 2 && T == 8, "row asm: 8-stripe tiles, 2 dwords per lane");
-            const u32 va = (u32)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)col;
-            ecgf::row_jt<K>(acc, va, w0, w1, w2, w3, k);
-            const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
-            if (ost != kNoSlot)
-                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
-            continue;
-        }
 #pragma unroll
         for (int b = 0; b < 8; ++b)
 #pragma unroll

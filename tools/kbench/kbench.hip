@@ -432,18 +432,12 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
      * default) against the round-1 per-plane trees ("naive"); the bit-pair
      * candidate kb_combine_bp lost in r01 and is no longer timed) */
     /* r02 (kbench_r02t.log and earlier): switch / naive / aligned / unrolled
-     * variants retired; the shipped jump table (jt) against the whole-row
-     * asm block of ec_gf8_row.h (row) */
+     * variants retired; r02z: the whole-row asm block ("row") and grouped
+     * waits ("split") were timed here (kbench_r02z_row.log, _split.log; code
+     * in commit 87d127c) and retired */
     add("TS1 NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 1, 4);
     add("TS1 NW8 NTS jt", ec_combine<K, 1, 8, false, true, 2, false, true, 1>, 1, 8);
     add("TS1 NW16 NTS jt", ec_combine<K, 1, 16, false, true, 2, false, true, 1>, 1, 16);
-    add("TS1 NW4 NTS row", ec_combine<K, 1, 4, false, true, 2, false, true, 3>, 1, 4);
-    add("TS1 NW8 NTS row", ec_combine<K, 1, 8, false, true, 2, false, true, 3>, 1, 8);
-    add("TS1 NW16 NTS row", ec_combine<K, 1, 16, false, true, 2, false, true, 3>, 1, 16);
-    /* grouped waits on the staged inputs (ec_combine SPLIT) */
-    if (K == 4)
-        add("TS1 NW8 NTS jt split", ec_combine<K, 1, 8, false, true, 2, false, true, 1, false, 1, true>, 1, 8);
-    add("TS1 NW16 NTS jt split", ec_combine<K, 1, 16, false, true, 2, false, true, 1, false, 1, true>, 1, 16);
     /* persistent double-buffered tiles: `bpc` blocks per CU */
     auto adddb = [&](const char *nm, auto kern, int nw, int bpc) {
         const size_t lds = 2 * (size_t)K * 8 * ECD_CHUNK;
@@ -654,9 +648,6 @@ int main(int argc, char **argv)
         addh("heal NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 4);
         addh("heal NW8 NTS", ec_combine<K, 1, 8, false, true>, 8);
         addh("heal NW16 NTS", ec_combine<K, 1, 16, false, true>, 16);
-        addh("heal NW4 NTS row", ec_combine<K, 1, 4, false, true, 2, false, true, 3>, 4);
-        addh("heal NW8 NTS row", ec_combine<K, 1, 8, false, true, 2, false, true, 3>, 8);
-        addh("heal NW4 NTS jt split", ec_combine<K, 1, 4, false, true, 2, false, true, 1, false, 1, true>, 4);
         run_group("heal 8+4 (regenerate 4 rows)", v, rounds, iters, s);
     }
     {   /* 16+4 decode, dense */
@@ -730,9 +721,6 @@ int main(int argc, char **argv)
         addm("mixed TS1 NW4 NTS jt", ec_combine<K, 1, 4, true, true, 2, false, true, 1>, 4);
         addm("mixed TS1 NW8 NTS", ec_combine<K, 1, 8, true, true>, 8);
         addm("mixed TS1 NW16 NTS", ec_combine<K, 1, 16, true, true>, 16);
-        addm("mixed TS1 NW8 NTS row", ec_combine<K, 1, 8, true, true, 2, false, true, 3>, 8);
-        addm("mixed TS1 NW4 NTS row", ec_combine<K, 1, 4, true, true, 2, false, true, 3>, 4);
-        addm("mixed TS1 NW8 NTS jt split", ec_combine<K, 1, 8, true, true, 2, false, true, 1, false, 1, true>, 8);
         run_group("decode 8+4 mixed (16 patterns, 1024-stripe groups)", v, rounds, iters, s);
     }
     if (!getenv("KB_NO_ENCODE")) {   /* encode 4+2, 8+4, 16+4: shipped W/NTS, CSE vs naive */
