@@ -197,13 +197,14 @@ int launch_encode_42_combine(hipStream_t s, uint64_t nstripes, const void *in, v
 
 } // namespace
 
-/* EC_MI355X_ENC=0 keeps the register-resident encoder for every geometry
- * (A/B runs only); unset = the shipped choice. */
-static bool enc_tiles()
+/* EC_MI355X_ENC=0 keeps the register-resident encoder for every geometry,
+ * =2 takes the tile encoders at every size (A/B runs only); unset = the
+ * shipped choice. */
+static int enc_mode()
 {
-    static const bool v = [] {
+    static const int v = [] {
         const char *e = getenv("EC_MI355X_ENC");
-        return !(e && *e == '0');
+        return e && (*e == '0' || *e == '2') ? *e - '0' : 1;
     }();
     return v;
 }
@@ -211,10 +212,10 @@ static bool enc_tiles()
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                        const void *in, void *const *out, bool zc)
 {
-    const bool tiles = !zc && enc_tiles();
+    const bool tiles = !zc && enc_mode() != 0;
     if (tiles && k == 4 && n == 6)
         return launch_encode_42_combine(s, nstripes, in, out);
-    if (tiles && k == 8 && n == 12 && nstripes > (1u << 17))
+    if (tiles && k == 8 && n == 12 && (nstripes > (1u << 17) || enc_mode() == 2))
         return launch_encode_tile<8, 12, 16, true, 2>(s, nstripes, in, out);
     if (tiles && k == 16 && n == 20)
         return launch_encode_tile<16, 20, 16, false, 1>(s, nstripes, in, out);
