@@ -340,6 +340,28 @@ int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+/* EC_MI355X_NW8 / EC_MI355X_NW4 = 4, 8 or 16: waves per block of every
+ * 4 < k <= 8 / k <= 4 combine, single and mixed patterns alike (tuning A/Bs
+ * only); unset = the shipped choice. */
+int nw_env(const char *name)
+{
+    const char *e = getenv(name);
+    const int n = e ? atoi(e) : 0;
+    return n == 4 || n == 8 || n == 16 ? n : 0;
+}
+
+int nw8_override()
+{
+    static const int v = nw_env("EC_MI355X_NW8");
+    return v;
+}
+
+int nw4_override()
+{
+    static const int v = nw_env("EC_MI355X_NW4");
+    return v;
+}
+
 /* Pattern groups of 1, 2 or 4 stripes: sort the stripes by pattern into
  * 8-slot tiles (ec_slots_*, ec_kernels_impl.h) and run the tile kernel over
  * the slot list.  Workspace: stream-ordered, freed after the launch. */
@@ -375,9 +397,11 @@ int launch_combine_slots(hipStream_t s, const CombineArgs &a0)
     }
     if (rc == 0) {
         if (a.k <= 4)
-            rc = launch_combine<4, 1, 8, 8, NTS, 1, 1, true>(s, a);
+            rc = nw4_override() == 16 ? launch_combine<4, 1, 16, 16, NTS, 1, 1, true>(s, a)
+                                      : launch_combine<4, 1, 8, 8, NTS, 1, 1, true>(s, a);
         else if (a.k <= 8)
-            rc = launch_combine<8, 1, 8, 8, NTS, 1, 1, true>(s, a);
+            rc = nw8_override() == 16 ? launch_combine<8, 1, 16, 16, NTS, 1, 1, true>(s, a)
+                                      : launch_combine<8, 1, 8, 8, NTS, 1, 1, true>(s, a);
         else
             rc = launch_combine<16, 1, 16, 16, NTS, 1, 1, true>(s, a);
     }
@@ -402,6 +426,22 @@ template <bool NTS>
 int launch_combine_k(hipStream_t s, const CombineArgs &a)
 {
     const int jt = jt_override();
+    if (a.k <= 4 && jt != 0 && !(a.group_pattern && a.group_shift < 3)) {
+        switch (nw4_override()) {
+        case 4: return launch_combine<4, 1, 4, 4, NTS, 1, 1>(s, a);
+        case 8: return launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
+        case 16: return launch_combine<4, 1, 16, 16, NTS, 1, 1>(s, a);
+        default: break;
+        }
+    }
+    if (a.k > 4 && a.k <= 8 && jt != 0 && !(a.group_pattern && a.group_shift < 3)) {
+        switch (nw8_override()) {
+        case 4: return launch_combine<8, 1, 4, 4, NTS, 1, 1>(s, a);
+        case 8: return launch_combine<8, 1, 8, 8, NTS, 1, 1>(s, a);
+        case 16: return launch_combine<8, 1, 16, 16, NTS, 1, 1>(s, a);
+        default: break;
+        }
+    }
     if (a.group_pattern && a.group_shift < 3)
         return launch_combine_slots<NTS>(s, a);
     /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
@@ -416,17 +456,20 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
         return sw ? launch_combine<4, 1, 8, 8, NTS, 0, 0>(s, a)
                : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
     if (a.k <= 8) {
-        /* Full decodes (rows > 4) of up to 128K stripes use 16-wave blocks:
-         * 64K-stripe batches (BASELINE configs[2]) 99.5 -> 91 us for 0xFF0,
-         * 108 -> 100 us for 0xEB5, same box, alternating libraries; at 1 GiB
-         * 4-wave blocks stay 2 % faster, at 128K stripes the two tie
-         * (profiles/kbench_r01_ts_*.log, ab_r01_nw16.log).  Heal-shaped
-         * calls (rows <= 4) keep 4 waves. */
-        if (a.rows > 4 && a.nstripes <= (1u << 17))
+        /* Full decodes (rows > 4) use 16-wave blocks, single and mixed
+         * patterns.  r01 (switch dispatch): 64K-stripe batches 99.5 -> 91 us
+         * for 0xFF0 against 4 waves, 1 GiB 2 % slower (ab_r01_nw16.log).
+         * r02z (jump table), same box through this launcher, EC_MI355X_NW8
+         * alternating (profiles/ab_nw8_r02z.log): 1 GiB 0.381-0.385 ms at 4
+         * waves -> 0.369-0.381 at 16; mixed patterns in 1024-stripe groups
+         * (BASELINE configs[4]) 0.449-0.466 ms at 8 waves -> 0.388-0.393 at
+         * 16; 64K-stripe 0xEB5 batches 16 ~ shipped, 8 and 4 slower.
+         * Heal-shaped calls (rows <= 4) keep 4 waves (all sizes tie). */
+        if (a.rows > 4)
             return sw ? launch_combine<8, 1, 16, 8, NTS, 0, 0>(s, a)
-                   : launch_combine<8, 1, 16, 8, NTS, 1, 1>(s, a);
+                      : launch_combine<8, 1, 16, 16, NTS, 1, 1>(s, a);
         return sw ? launch_combine<8, 1, 4, 8, NTS, 0, 0>(s, a)
-               : launch_combine<8, 1, 4, 8, NTS, 1, 1>(s, a);
+                  : launch_combine<8, 1, 4, 16, NTS, 1, 1>(s, a);
     }
     return sw ? launch_combine<16, 1, 16, 16, NTS, 0, 0>(s, a)
            : launch_combine<16, 1, 16, 16, NTS, 1, 1>(s, a);

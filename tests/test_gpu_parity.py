@@ -434,8 +434,9 @@ def test_decode_device_every_mask_16p4(ec, oracle, torch_cuda):
 
 @pytest.mark.parametrize("mask", [0xFF0, 0xEB5])
 def test_decode_device_8p4_large_batch(ec, oracle, torch_cuda, mask):
-    """More than 131,072 stripes of 8+4: the 4-wave-block instantiation the
-    launcher picks for large full decodes (ec_kernels.hip launch_combine_k)."""
+    """More than 131,072 stripes of 8+4 (a full decode past the 128K-stripe
+    switch of round 1; since r02z every 8+4 full decode runs the 16-wave
+    instantiation, ec_kernels.hip launch_combine_k)."""
     _device_decode_masks(ec, oracle, torch_cuda, 8, 12, [mask], (1 << 17) + 77, seed=812,
                          nthreads=8)
 
