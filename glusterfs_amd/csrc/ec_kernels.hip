@@ -396,12 +396,17 @@ int launch_combine_slots(hipStream_t s, const CombineArgs &a0)
         rc = hipGetLastError() == hipSuccess ? 0 : -EIO;
     }
     if (rc == 0) {
+        /* waves per block: 4 for k <= 4 (1-/4-stripe groups of 4+2 0.49 ->
+         * 0.45 ms per GiB against 8), 8 for k <= 8 (4 and 16 slower), same
+         * box through this launcher (profiles/ab_slots_r02z.log) */
         if (a.k <= 4)
-            rc = nw4_override() == 16 ? launch_combine<4, 1, 16, 16, NTS, 1, 1, true>(s, a)
-                                      : launch_combine<4, 1, 8, 8, NTS, 1, 1, true>(s, a);
+            rc = nw4_override() == 16  ? launch_combine<4, 1, 16, 16, NTS, 1, 1, true>(s, a)
+                 : nw4_override() == 8 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, true>(s, a)
+                                       : launch_combine<4, 1, 4, 4, NTS, 1, 1, true>(s, a);
         else if (a.k <= 8)
-            rc = nw8_override() == 16 ? launch_combine<8, 1, 16, 16, NTS, 1, 1, true>(s, a)
-                                      : launch_combine<8, 1, 8, 8, NTS, 1, 1, true>(s, a);
+            rc = nw8_override() == 16  ? launch_combine<8, 1, 16, 16, NTS, 1, 1, true>(s, a)
+                 : nw8_override() == 4 ? launch_combine<8, 1, 4, 4, NTS, 1, 1, true>(s, a)
+                                       : launch_combine<8, 1, 8, 8, NTS, 1, 1, true>(s, a);
         else
             rc = launch_combine<16, 1, 16, 16, NTS, 1, 1, true>(s, a);
     }
