@@ -340,9 +340,9 @@ int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-/* EC_MI355X_NW8 / EC_MI355X_NW4 = 4, 8 or 16: waves per block of every
- * 4 < k <= 8 / k <= 4 combine, single and mixed patterns alike (tuning A/Bs
- * only); unset = the shipped choice. */
+/* EC_MI355X_NW4 / _NW8 / _NW16 = 4, 8 or 16: waves per block of every
+ * k <= 4 / 4 < k <= 8 / k > 8 combine, single and mixed patterns alike
+ * (tuning A/Bs only); unset = the shipped choice. */
 int nw_env(const char *name)
 {
     const char *e = getenv(name);
@@ -359,6 +359,12 @@ int nw8_override()
 int nw4_override()
 {
     static const int v = nw_env("EC_MI355X_NW4");
+    return v;
+}
+
+int nw16_override()
+{
+    static const int v = nw_env("EC_MI355X_NW16");
     return v;
 }
 
@@ -444,6 +450,13 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
         case 4: return launch_combine<8, 1, 4, 4, NTS, 1, 1>(s, a);
         case 8: return launch_combine<8, 1, 8, 8, NTS, 1, 1>(s, a);
         case 16: return launch_combine<8, 1, 16, 16, NTS, 1, 1>(s, a);
+        default: break;
+        }
+    }
+    if (a.k > 8 && jt != 0 && !(a.group_pattern && a.group_shift < 3)) {
+        switch (nw16_override()) {
+        case 4: return launch_combine<16, 1, 4, 4, NTS, 1, 1>(s, a);
+        case 8: return launch_combine<16, 1, 8, 8, NTS, 1, 1>(s, a);
         default: break;
         }
     }
