@@ -490,14 +490,14 @@ static uint8_t kb_gmul(uint8_t a, uint8_t b)
 
 /* Encode through the generic tile kernel (LDS-DMA staging, NT stores):
  * rows = n, coefficient (i+1)^(k-1-j) for input j (ec-method.c:22-36). */
-template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2>
+template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2, int RB = 1>
 static void add_encode_tile(std::vector<Variant> &vars, const char *nm, uint64_t nst,
                             const uint8_t *in, const FragPtrs &f)
 {
     const size_t lds = (size_t)K * 8 * ECD_CHUNK;
     const uint64_t g = (nst + 7) / 8;
     vars.push_back({nm, (double)nst * (K + N) * ECD_CHUNK, [=](hipStream_t st) {
-                        hipLaunchKernelGGL((ec_encode_tile<K, N, NW, NTS, DIRECT, CW>), dim3((u32)g),
+                        hipLaunchKernelGGL((ec_encode_tile<K, N, NW, NTS, DIRECT, CW, RB>), dim3((u32)g),
                                            dim3(64 * NW), lds, st, in, f, nst);
                     }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
 }
@@ -588,7 +588,7 @@ int main(int argc, char **argv)
                      }, nullptr, 0});
         run_group("HBM calibration", v, rounds, iters, s);
     }
-    {   /* 4+2 decode */
+    if (!getenv("KB_NO_DECODE")) {   /* 4+2 decode */
         const uint64_t nst = user / (4 * ECD_CHUNK);
         uint8_t *fr[4];
         for (int p = 0; p < 4; ++p)
@@ -599,7 +599,7 @@ int main(int argc, char **argv)
         add_decode<4>(v, nst, fr, bufB, inv);
         run_group("decode 4+2 mask 0x3C", v, rounds, iters, s);
     }
-    {   /* 8+4 decode: a dense pseudo-random nonzero matrix */
+    if (!getenv("KB_NO_DECODE")) {   /* 8+4 decode: a dense pseudo-random nonzero matrix */
         const uint64_t nst = user / (8 * ECD_CHUNK);
         uint8_t *fr[8];
         for (int p = 0; p < 8; ++p)
@@ -611,7 +611,7 @@ int main(int argc, char **argv)
         add_decode<8>(v, nst, fr, bufB, c);
         run_group("decode 8+4 dense", v, rounds, iters, s);
     }
-    {   /* 8+4 fused heal shape: k = 8 inputs, 4 output rows */
+    if (!getenv("KB_NO_DECODE")) {   /* 8+4 fused heal shape: k = 8 inputs, 4 output rows */
         const int K = 8, RW = 4;
         const uint64_t nst = user / (K * ECD_CHUNK);
         ecd_combine_desc_t d;
@@ -650,7 +650,7 @@ int main(int argc, char **argv)
         addh("heal NW16 NTS", ec_combine<K, 1, 16, false, true>, 16);
         run_group("heal 8+4 (regenerate 4 rows)", v, rounds, iters, s);
     }
-    {   /* 16+4 decode, dense */
+    if (!getenv("KB_NO_DECODE")) {   /* 16+4 decode, dense */
         const uint64_t nst = user / (16 * ECD_CHUNK);
         uint8_t *fr[16];
         for (int p = 0; p < 16; ++p)
@@ -662,7 +662,7 @@ int main(int argc, char **argv)
         add_decode<16>(v, nst, fr, bufB, c);
         run_group("decode 16+4 dense", v, rounds, iters, s);
     }
-    {   /* 8+4 mixed: 16 random dense patterns over 12 fragments, 1024-stripe groups */
+    if (!getenv("KB_NO_DECODE")) {   /* 8+4 mixed: 16 random dense patterns over 12 fragments, 1024-stripe groups */
         const int K = 8, N = 12, NP = 16;
         const uint64_t nst = user / (K * ECD_CHUNK);
         ecd_combine_desc_t d;
@@ -758,6 +758,10 @@ int main(int argc, char **argv)
         add_encode_tile<8, 12, 16, true, true>(v, "enc 8+4 vtile NW16 NTS direct", nst, bufA, f);
         add_encode_tile<8, 12, 16, true, false, 1>(v, "enc 8+4 vtile NW16 NTS CW1", nst, bufA, f);
         add_encode_tile<8, 12, 16, true, true, 1>(v, "enc 8+4 vtile NW16 NTS direct CW1", nst, bufA, f);
+        add_encode_tile<8, 12, 12, true, false, 1, 2>(v, "enc 8+4 vtile NW12 CW1 RB2", nst, bufA, f);
+        add_encode_tile<8, 12, 8, true, false, 1, 3>(v, "enc 8+4 vtile NW8 CW1 RB3", nst, bufA, f);
+        add_encode_tile<8, 12, 6, true, false, 2, 2>(v, "enc 8+4 vtile NW6 CW2 RB2", nst, bufA, f);
+        add_encode_tile<8, 12, 12, true, false, 2, 2>(v, "enc 8+4 vtile NW12 CW2 RB2", nst, bufA, f);
         run_group("encode 8+4", v, rounds, iters, s);
         v.clear();
         {   /* configs[2]: one 64K-stripe batch */
@@ -783,6 +787,12 @@ int main(int argc, char **argv)
         add_encode_tile<16, 20, 16, true, false, 1>(v, "enc 16+4 vtile NW16 NTS CW1", nst, bufA, f);
         add_encode_tile<16, 20, 16, true, true, 1>(v, "enc 16+4 vtile NW16 NTS direct CW1", nst, bufA, f);
         add_encode_tile<16, 20, 16, true, true, 2>(v, "enc 16+4 vtile NW16 NTS direct", nst, bufA, f);
+        /* r02z: row groups (RB rows per wave item share each LDS read) */
+        add_encode_tile<16, 20, 10, true, false, 1, 2>(v, "enc 16+4 vtile NW10 CW1 RB2", nst, bufA, f);
+        add_encode_tile<16, 20, 16, true, false, 1, 2>(v, "enc 16+4 vtile NW16 CW1 RB2", nst, bufA, f);
+        add_encode_tile<16, 20, 10, true, false, 1, 4>(v, "enc 16+4 vtile NW10 CW1 RB4", nst, bufA, f);
+        add_encode_tile<16, 20, 10, true, false, 2, 2>(v, "enc 16+4 vtile NW10 CW2 RB2", nst, bufA, f);
+        add_encode_tile<16, 20, 5, true, false, 2, 4>(v, "enc 16+4 vtile NW5 CW2 RB4", nst, bufA, f);
         run_group("encode 16+4", v, rounds, iters, s);
     }
     if (!getenv("KB_NO_RMW")) {   /* partial-stripe write: interior stripes read at an odd address */
