@@ -281,56 +281,10 @@ __device__ __forceinline__ void encode_tile_row(const uint8_t *col, uint8_t *dst
     store_chunk<CW, NTS>(dst, acc);
 }
 
-/* RB > 1: one wave item computes RB consecutive rows I0 .. I0+RB-1 (Horner),
- * so each input plane read from LDS feeds RB rows instead of one: the
- * 16+4 tile reads 5120 ds_read_b32 per 8 stripes at RB = 1, CW = 1. */
-template <int K, int I0, int RB, bool NTS, int CW>
-__device__ __forceinline__ void encode_tile_rows(const uint8_t *col, const FragPtrs &out,
-                                                 uint64_t off)
-{
-    constexpr u32 T = 8;
-    u32 acc[RB][8][CW], y[8][CW];
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-        load_plane<CW>(col + (u32)b * (T * 64u), y[b]);
-#pragma unroll
-    for (int q = 0; q < RB; ++q)
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-#pragma unroll
-            for (int w = 0; w < CW; ++w)
-                acc[q][b][w] = y[b][w];
-#pragma unroll
-    for (int j = 1; j < K; ++j) {
-        const uint8_t *src = col + (u32)j * (T * ECD_CHUNK);
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-            load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
-        static_for<0, RB>([&](auto Q) {
-            constexpr int q = decltype(Q)::value;
-            constexpr u32 v = I0 + q + 1;
-            if constexpr (v == 1) {
-#pragma unroll
-                for (int b = 0; b < 8; ++b)
-#pragma unroll
-                    for (int w = 0; w < CW; ++w)
-                        acc[q][b][w] ^= y[b][w];
-            } else {
-                ecgf::horner<v, CW, true>(acc[q], y);
-            }
-        });
-    }
-    static_for<0, RB>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        store_chunk<CW, NTS>(out.p[I0 + q] + off, acc[q]);
-    });
-}
-
-template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2, int RB = 1>
+template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2>
 __global__ __launch_bounds__(NW * 64) void ec_encode_tile(const uint8_t *__restrict__ in,
                                                           const FragPtrs out, uint64_t nstripes)
 {
-    static_assert(RB == 1 || (N % RB == 0 && !DIRECT), "row groups: Horner, RB | N");
     constexpr u32 T = 8;
     constexpr uint64_t S = (uint64_t)K * ECD_CHUNK;
     constexpr u32 NI = K * T * 32 / 64;      /* LDS-DMA wave instructions per tile */
@@ -361,21 +315,6 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile(const uint8_t *__restr
     __syncthreads();
 
     const u32 cs = lane / LPS, cc = lane % LPS;
-    if constexpr (RB > 1) {
-        for (u32 it = wave; it < (u32)(N / RB) * IPR; it += NW) {
-            const u32 g = __builtin_amdgcn_readfirstlane(it / IPR);
-            const u32 s = (it % IPR) * SPI + cs;
-            const uint64_t ost = t0 + s;
-            const uint8_t *col = lds + s * 64u + cc * (4u * CW);
-            if (ost < nstripes)
-                static_for<0, N / RB>([&](auto G) {
-                    if (g == (u32)decltype(G)::value)
-                        encode_tile_rows<K, decltype(G)::value * RB, RB, NTS, CW>(
-                            col, out, ost * ECD_CHUNK + cc * (4u * CW));
-                });
-        }
-        return;
-    }
     for (u32 it = wave; it < (u32)N * IPR; it += NW) {
         const u32 r = __builtin_amdgcn_readfirstlane(it / IPR);
         const u32 s = (it % IPR) * SPI + cs;

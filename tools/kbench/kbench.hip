@@ -490,14 +490,14 @@ static uint8_t kb_gmul(uint8_t a, uint8_t b)
 
 /* Encode through the generic tile kernel (LDS-DMA staging, NT stores):
  * rows = n, coefficient (i+1)^(k-1-j) for input j (ec-method.c:22-36). */
-template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2, int RB = 1>
+template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2>
 static void add_encode_tile(std::vector<Variant> &vars, const char *nm, uint64_t nst,
                             const uint8_t *in, const FragPtrs &f)
 {
     const size_t lds = (size_t)K * 8 * ECD_CHUNK;
     const uint64_t g = (nst + 7) / 8;
     vars.push_back({nm, (double)nst * (K + N) * ECD_CHUNK, [=](hipStream_t st) {
-                        hipLaunchKernelGGL((ec_encode_tile<K, N, NW, NTS, DIRECT, CW, RB>), dim3((u32)g),
+                        hipLaunchKernelGGL((ec_encode_tile<K, N, NW, NTS, DIRECT, CW>), dim3((u32)g),
                                            dim3(64 * NW), lds, st, in, f, nst);
                     }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
 }
@@ -758,10 +758,6 @@ int main(int argc, char **argv)
         add_encode_tile<8, 12, 16, true, true>(v, "enc 8+4 vtile NW16 NTS direct", nst, bufA, f);
         add_encode_tile<8, 12, 16, true, false, 1>(v, "enc 8+4 vtile NW16 NTS CW1", nst, bufA, f);
         add_encode_tile<8, 12, 16, true, true, 1>(v, "enc 8+4 vtile NW16 NTS direct CW1", nst, bufA, f);
-        add_encode_tile<8, 12, 12, true, false, 1, 2>(v, "enc 8+4 vtile NW12 CW1 RB2", nst, bufA, f);
-        add_encode_tile<8, 12, 8, true, false, 1, 3>(v, "enc 8+4 vtile NW8 CW1 RB3", nst, bufA, f);
-        add_encode_tile<8, 12, 6, true, false, 2, 2>(v, "enc 8+4 vtile NW6 CW2 RB2", nst, bufA, f);
-        add_encode_tile<8, 12, 12, true, false, 2, 2>(v, "enc 8+4 vtile NW12 CW2 RB2", nst, bufA, f);
         run_group("encode 8+4", v, rounds, iters, s);
         v.clear();
         {   /* configs[2]: one 64K-stripe batch */
@@ -787,12 +783,8 @@ int main(int argc, char **argv)
         add_encode_tile<16, 20, 16, true, false, 1>(v, "enc 16+4 vtile NW16 NTS CW1", nst, bufA, f);
         add_encode_tile<16, 20, 16, true, true, 1>(v, "enc 16+4 vtile NW16 NTS direct CW1", nst, bufA, f);
         add_encode_tile<16, 20, 16, true, true, 2>(v, "enc 16+4 vtile NW16 NTS direct", nst, bufA, f);
-        /* r02z: row groups (RB rows per wave item share each LDS read) */
-        add_encode_tile<16, 20, 10, true, false, 1, 2>(v, "enc 16+4 vtile NW10 CW1 RB2", nst, bufA, f);
-        add_encode_tile<16, 20, 16, true, false, 1, 2>(v, "enc 16+4 vtile NW16 CW1 RB2", nst, bufA, f);
-        add_encode_tile<16, 20, 10, true, false, 1, 4>(v, "enc 16+4 vtile NW10 CW1 RB4", nst, bufA, f);
-        add_encode_tile<16, 20, 10, true, false, 2, 2>(v, "enc 16+4 vtile NW10 CW2 RB2", nst, bufA, f);
-        add_encode_tile<16, 20, 5, true, false, 2, 4>(v, "enc 16+4 vtile NW5 CW2 RB4", nst, bufA, f);
+        /* r02z: row groups (RB rows per wave item sharing each LDS read) were
+         * timed here and retired: kbench_r02z_rb.log, code in commit 822a197 */
         run_group("encode 16+4", v, rounds, iters, s);
     }
     if (!getenv("KB_NO_RMW")) {   /* partial-stripe write: interior stripes read at an odd address */
