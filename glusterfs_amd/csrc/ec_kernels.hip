@@ -317,27 +317,155 @@ __global__ __launch_bounds__(256) void ec_pat_upload(const PatChunk c)
         c.dst[i] = c.w[i];
 }
 
-/* Mixed calls whose patterns exceed the 2 KiB argument space: a per-call
- * device table (stream-ordered allocation, freed after the combine). */
-int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32 **tab)
+/* Enqueue the upload of `w` into the device table `tab` on `s`. */
+int enqueue_upload(hipStream_t s, const std::vector<u32> &w, u32 *tab)
+{
+    PatChunk c;
+    for (size_t o = 0; o < w.size(); o += kPatWords) {
+        c.dst = tab + o;
+        c.n = (u32)std::min<size_t>(kPatWords, w.size() - o);
+        memcpy(c.w, w.data() + o, (size_t)c.n * 4);
+        hipLaunchKernelGGL(ec_pat_upload, dim3(1), dim3(256), 0, s, c);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+/* Mixed calls whose patterns exceed the 2 KiB argument space read their
+ * decode matrices from a device table.  A self-heal sweep passes the same
+ * mask set call after call, so the tables of recent calls stay on the
+ * device (per device, LRU): a repeated call skips the allocation and the
+ * upload launches (one per 2 KiB: ~9 for 64 masks of 16+4, ~50 us of
+ * stream time per call).  An entry is reused only for identical words, and
+ * evicted (LRU, after the device drains) only when no call holds it. */
+class PatTableCache {
+  public:
+    struct Ref {
+        int slot = -1;
+        u32 *ptr = nullptr;
+    };
+
+    /* A table holding `w` on the current device, ordered before work that
+     * `s` runs after this call; release() it once that work is enqueued. */
+    int acquire(hipStream_t s, const std::vector<u32> &w, Ref &ref)
+    {
+        static const bool off = [] {   /* EC_MI355X_PATCACHE=0: per-call tables (A/B) */
+            const char *e = getenv("EC_MI355X_PATCACHE");
+            return e && *e == '0';
+        }();
+        if (off)
+            return -EBUSY;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess)
+            return -EIO;
+        uint64_t h = 1469598103934665603ull;     /* FNV-1a over the words */
+        for (u32 x : w)
+            h = (h ^ x) * 1099511628211ull;
+        std::lock_guard<std::mutex> g(mu_);
+        int victim = -1;
+        for (int i = 0; i < kEntries; ++i) {
+            Entry &e = e_[i];
+            if (e.ptr && e.dev == dev && e.hash == h && e.words == w) {
+                ++e.inflight;
+                e.tick = ++tick_;
+                ref.slot = i;
+                ref.ptr = e.ptr;
+                return hipStreamWaitEvent(s, e.ready, 0) == hipSuccess ? 0 : -EIO;
+            }
+            if (e.inflight == 0 && (e.dev == dev || !e.ptr) &&
+                (victim < 0 || !e.ptr || (e_[victim].ptr && e.tick < e_[victim].tick)))
+                victim = i;
+        }
+        if (victim < 0)
+            return -EBUSY;                    /* every entry in use: per call */
+        Entry &e = e_[victim];
+        if (e.ptr) {
+            /* evict: its readers may sit on several callers' streams, so
+             * wait for the whole device (rare: > kEntries live mask sets) */
+            (void)hipDeviceSynchronize();
+            (void)hipFree(e.ptr);
+            e.ptr = nullptr;
+        }
+        if (e.dev != dev) {
+            if (e.ready)
+                (void)hipEventDestroy(e.ready);
+            e.ready = nullptr;
+            if (hipEventCreateWithFlags(&e.ready, hipEventDisableTiming) != hipSuccess) {
+                (void)hipGetLastError();
+                return -EIO;
+            }
+            e.dev = dev;
+        }
+        if (hipMalloc(reinterpret_cast<void **>(&e.ptr), w.size() * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            e.ptr = nullptr;
+            return -ENOMEM;
+        }
+        if (enqueue_upload(s, w, e.ptr) != 0 || hipEventRecord(e.ready, s) != hipSuccess) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(e.ptr);
+            e.ptr = nullptr;
+            return -EIO;
+        }
+        e.hash = h;
+        e.words = w;
+        e.inflight = 1;
+        e.tick = ++tick_;
+        ref.slot = victim;
+        ref.ptr = e.ptr;
+        return 0;
+    }
+
+    /* The work that reads the table has been enqueued. */
+    void release(const Ref &ref)
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        --e_[ref.slot].inflight;
+    }
+
+  private:
+    struct Entry {
+        int dev = -1;
+        uint64_t hash = 0, tick = 0;
+        std::vector<u32> words;
+        u32 *ptr = nullptr;
+        hipEvent_t ready = nullptr;           /* the upload has landed */
+        int inflight = 0;
+    };
+    static constexpr int kEntries = 16;
+    std::mutex mu_;
+    Entry e_[kEntries];
+    uint64_t tick_ = 0;
+};
+
+/* never destroyed: tables and events would be freed after the runtime */
+PatTableCache &pat_tables()
+{
+    static PatTableCache *c = new PatTableCache;
+    return *c;
+}
+
+/* The device table of a mixed call: from the cache, or (all entries busy)
+ * a per-call table (stream-ordered allocation, freed after the combine). */
+int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32 **tab,
+                 PatTableCache::Ref &ref)
 {
     const size_t nw = (size_t)a.pwords * a.npatterns;
     std::vector<u32> w(nw, 0u);
     pack_words(d, a.kw, a.pwords, w.data());
+    const int rc = pat_tables().acquire(s, w, ref);
+    if (rc == 0) {
+        a.patg = ref.ptr;
+        return 0;
+    }
+    if (rc != -EBUSY)
+        return rc;
     if (hipMallocAsync(reinterpret_cast<void **>(tab), nw * 4, s) != hipSuccess) {
         *tab = nullptr;
         (void)hipGetLastError();
         return -ENOMEM;
     }
-    PatChunk c;
-    for (size_t o = 0; o < nw; o += kPatWords) {
-        c.dst = *tab + o;
-        c.n = (u32)std::min<size_t>(kPatWords, nw - o);
-        memcpy(c.w, w.data() + o, (size_t)c.n * 4);
-        hipLaunchKernelGGL(ec_pat_upload, dim3(1), dim3(256), 0, s, c);
-    }
     a.patg = *tab;
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return enqueue_upload(s, w, *tab);
 }
 
 /* EC_MI355X_NW4 / _NW8 / _NW16 = 4, 8 or 16: waves per block of every
@@ -500,10 +628,13 @@ int combine_any(hipStream_t s, const ecd_combine_desc_t *d)
     CombineArgs a;
     int rc = ecdk_pack_args(d, &a);
     u32 *tab = nullptr;
+    PatTableCache::Ref ref;
     if (rc == -E2BIG && d->group_pattern)
-        rc = upload_table(s, d, a, &tab);
+        rc = upload_table(s, d, a, &tab, ref);
     if (rc == 0)
         rc = launch_combine_k<NTS>(s, a);
+    if (ref.slot >= 0)
+        pat_tables().release(ref);
     if (tab)
         (void)hipFreeAsync(tab, s);
     return rc;

@@ -294,6 +294,51 @@ def test_decode_mixed_too_many_patterns(ec, oracle):
         assert ei.value.errno == errno.E2BIG
 
 
+def test_mixed_device_table_cache(ec, oracle, torch_cuda):
+    """Mixed decodes past the argument space reuse their device table across
+    calls (ec_kernels.hip PatTableCache, 16 entries per device): 20 distinct
+    sets of 12 masks of 16+4, cycled twice, so later calls hit entries and
+    others evict them, and two threads on their own streams decode the same
+    set concurrently.  Random fragments: every group is compared with the
+    oracle's inverse."""
+    import threading
+    torch = torch_cuda
+    k, n, group, per = 16, 20, 8, 12
+    sets = [_distinct_masks(n, k, per, seed=300 + i) for i in range(20)]
+    nst = group * per
+    frags = [rand_bytes(CHUNK * nst, seed=900 + f) for f in range(n)]
+    dfr = [torch.from_numpy(f).cuda() for f in frags]
+    gp = torch.arange(per, dtype=torch.uint8, device="cuda")
+    with ec.ECMatrixList(k, n) as L:
+        for rep in range(2):
+            for masks in sets:
+                out = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+                L.decode_mixed_device(0, None, nst, group, gp, masks, dfr, out)
+                ec.sync_device(0)
+                _check_groups(oracle, k, group, nst, masks, frags, out.cpu().numpy())
+        outs, errs = {}, []
+
+        def worker(t):
+            try:
+                st = torch.cuda.Stream()
+                o = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+                for _ in range(10):
+                    L.decode_mixed_device(0, st.cuda_stream, nst, group, gp, sets[t % 3], dfr, o)
+                st.synchronize()
+                outs[t] = o.cpu().numpy()
+            except Exception as e:                 # reported below
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        for t, o in outs.items():
+            _check_groups(oracle, k, group, nst, sets[t % 3], frags, o)
+
+
 def _check_groups(oracle, k, group, nst, masks, frags, out):
     for g, m in enumerate(masks):
         s0, s1 = g * group, min((g + 1) * group, nst)
