@@ -680,7 +680,12 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
 
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
 {
-    return combine_any<true>(s, d);
+    /* EC_MI355X_NTS=0: default-policy stores on the device path (A/B only) */
+    static const bool nts = [] {
+        const char *e = getenv("EC_MI355X_NTS");
+        return !(e && *e == '0');
+    }();
+    return nts ? combine_any<true>(s, d) : combine_any<false>(s, d);
 }
 
 /* Host-buffer path: every buffer is pinned host memory read / written over
