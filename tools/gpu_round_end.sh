@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-end evidence at HEAD (one gpurun call): smoke -> GPU tests -> the
+# driver's bench command -> rocprofv3 kernel stats of the same command's
+# headline (--no-extra --no-cpu) -> 2-rank rehearsal (gloo, both ranks on
+# GPU 0) -> per-config rocprof + PMC passes.  Stops at the first failure.
+set -u
+mkdir -p gpurun_out
+TAG=${TAG:-round_end}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "[$(date +%T)] start $name"
+  timeout -k 10 "$to" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"; tail -3 "gpurun_out/${TAG}_$name.log" | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+run pytest_gpu 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+run bench 400 python -u bench.py --gpus 1 --steps 20 --warmup 5
+run bench_rocprof 300 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_bench_$TAG -o run --output-format csv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-extra --no-cpu && python3 $R/tools/prof_filter.py $R/gpurun_out/prof_bench_$TAG ec_"
+run rehearsal 300 env EC_BENCH_BACKEND=gloo EC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1
+run profile 900 bash tools/profile.sh "$TAG" dec:4+2:3C 1 enc:4+2 1 enc:8+4 0.25 dec:8+4:FF0 0.25 \
+  enc:16+4 2 mixed:8+4 1 heal:8+4 1 dec:16+4:FFFF0 1 mixed:16+4:64 1 rmw:4+2 1
+echo "[$(date +%T)] done"
