@@ -26,7 +26,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifndef MAXT
 #define MAXT 8
+#endif
 #define BEAM 96
 #define MAXS (8 + MAXT)
 

@@ -390,6 +390,84 @@ __global__ __launch_bounds__(NW * 64) void kb_combine_db(const CombineArgs a)
     }
 }
 
+/* Candidate (r02z): ec_combine with the next input's LDS reads issued before
+ * the current multiply (software pipelining), so the LDS latency overlaps
+ * the dispatch and the body instead of heading every multiply.  The second
+ * 16-VGPR input buffer fits the 64-VGPR budget (two 16-wave blocks per CU)
+ * only with programs of at most 4 temporaries (gf8_asm_t4.h).  Zero
+ * coefficients go through table entry 0 (a no-op body). */
+#include "gf8_asm_t4.h"
+
+template <int K, int NW, bool NTS>
+__global__ __launch_bounds__(NW * 64) void kb_combine_pf(const CombineArgs a)
+{
+    constexpr u32 T = 8;
+    constexpr u32 NI = K * T * 32 / 64;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const PatWords<false> pw(a, 0u, lane, nullptr);
+#pragma unroll
+    for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
+        const u32 ins = j * NW + wave;
+        if (ins >= NI)
+            break;
+        const u32 p = ins / (T / 2);
+        if (p >= k)
+            break;
+        const u32 el = (ins * 64 + lane) % (T * 32);
+        const u32 s = (el >> 2) % T;
+        const uint64_t st = t0 + s;
+        if (st < a.nstripes) {
+            const uint8_t *g = a.in_base[pw.byte(a, p)] + st * a.in_stride +
+                               ((el >> 2) / T) * 64u + (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+        }
+    }
+    __syncthreads();
+    const u32 cs = lane >> 3, cc = lane & 7u;
+    for (u32 r = wave; r < a.rows; r += NW) {
+        const uint8_t *col = lds + cs * 64u + cc * 8u;
+        const u32 rw = a.kw * (1 + r);
+        const u32 w0 = pw.word(a, rw);
+        const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+        const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
+        const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
+        u32 acc[8][2], ya[8][2], yb[8][2], t[ECGF_ASM_TEMPS_T4][2];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            acc[b][0] = acc[b][1] = 0;
+            load_plane<2>(col + (u32)b * (T * 64u), ya[b]);
+        }
+        uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
+#pragma unroll 1
+        for (u32 p = 0; p < k; ++p) {
+            const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+            cl = (cl >> 8) | (ch << 56);
+            ch >>= 8;
+            const uint8_t *nx = col + (p + 1 < k ? p + 1 : p) * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<2>(nx + (u32)b * (T * 64u), yb[b]);
+            ECGF_ASM_DISPATCH_W2_T4(acc, ya, t, c);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                ya[b][0] = yb[b][0];
+                ya[b][1] = yb[b][1];
+            }
+        }
+        const uint64_t ost = t0 + cs;
+        if (ost < a.nstripes)
+            store_chunk<2, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+    }
+}
+
 /* decode k+r with the first r bricks missing, coefficients from the host
  * inverse (a dense k x k matrix is all we need for timing; correctness of
  * the math is covered by the parity tests -- here variants are compared
@@ -438,6 +516,9 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     add("TS1 NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 1, 4);
     add("TS1 NW8 NTS jt", ec_combine<K, 1, 8, false, true, 2, false, true, 1>, 1, 8);
     add("TS1 NW16 NTS jt", ec_combine<K, 1, 16, false, true, 2, false, true, 1>, 1, 16);
+    /* r02z: next input's LDS reads issued before the current multiply */
+    add("TS1 NW8 NTS pf", kb_combine_pf<K, 8, true>, 1, 8);
+    add("TS1 NW16 NTS pf", kb_combine_pf<K, 16, true>, 1, 16);
     /* persistent double-buffered tiles: `bpc` blocks per CU */
     auto adddb = [&](const char *nm, auto kern, int nw, int bpc) {
         const size_t lds = 2 * (size_t)K * 8 * ECD_CHUNK;
