@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "ec_gf8_asm.h"
+#include "ec_gf8_asm_t4.h"
 #include "ec_gf8_prog.h"
 
 namespace ecgf {
@@ -199,6 +200,14 @@ __device__ __forceinline__ void mul_xor_jt(u32 c, u32 (&acc)[8][W], const u32 (&
         ECGF_ASM_DISPATCH_W2_A32(acc, x, t, c);  /* bodies on 32-byte boundaries */
     else
         ECGF_ASM_DISPATCH_W2(acc, x, t, c);
+}
+
+/* The same with the <= 4-temporary programs of ec_gf8_asm_t4.h (8 VGPRs of
+ * temporaries instead of 12: room for a second input buffer). */
+__device__ __forceinline__ void mul_xor_jt4(u32 c, u32 (&acc)[8][2], const u32 (&x)[8][2])
+{
+    u32 t[ECGF_ASM_TEMPS_T4][2];
+    ECGF_ASM_DISPATCH_W2_T4(acc, x, t, c);
 }
 
 } // namespace ecgf

@@ -556,7 +556,7 @@ int jt_override()
 {
     static const int v = [] {
         const char *e = getenv("EC_MI355X_JT");
-        return e && (*e == '0' || *e == '1') ? *e - '0' : -1;
+        return e && (*e == '0' || *e == '1' || *e == '4') ? *e - '0' : -1;
     }();
     return v;
 }
@@ -598,6 +598,13 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
      * 8+4 64K-stripe batches and 8+4 mixed ties.  EC_MI355X_JT=0 keeps the
      * compiler's switch for A/Bs. */
     const bool sw = jt == 0;
+    if (jt == 4 && a.k <= 8) {     /* software-pipelined loop (A/B) */
+        if (a.k <= 4)
+            return launch_combine<4, 1, 8, 8, NTS, 4, 4>(s, a);
+        if (a.rows > 4)
+            return launch_combine<8, 1, 16, 16, NTS, 4, 4>(s, a);
+        return launch_combine<8, 1, 4, 16, NTS, 4, 4>(s, a);
+    }
     if (a.k <= 4)
         return sw ? launch_combine<4, 1, 8, 8, NTS, 0, 0>(s, a)
                : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);

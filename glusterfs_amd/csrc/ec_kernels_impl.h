@@ -556,7 +556,8 @@ __device__ __forceinline__ uint64_t slot_stripe(const CombineArgs &a, uint64_t s
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
 /* JT: 0 = the compiler's switch, 1 = the jump table of ec_gf8_asm.h, 2 = the
- * same with 32-byte-aligned bodies.  (r02z also A/B'd a whole-row asm block
+ * same with 32-byte-aligned bodies, 4 = a software-pipelined loop over the
+ * <= 4-temporary programs of ec_gf8_asm_t4.h.  (r02z also A/B'd a whole-row asm block
  * and grouped waits on the staged inputs; neither was faster: DESIGN.md 3.4,
  * code in commit 87d127c.)
  * SLOTS: mixed patterns with groups below a tile (1, 2, 4 stripes): the
@@ -627,6 +628,40 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
         const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
         u32 acc[8][CW], y[8][CW];
+        if constexpr (JT == 4) {
+            /* software-pipelined: the next input's planes are read from LDS
+             * before the current multiply, so their latency overlaps the
+             * dispatch and the body; zero coefficients run table entry 0 */
+            static_assert(CW == 2, "pipelined loop: 2 dwords per lane");
+            u32 yn[8][2];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                acc[b][0] = acc[b][1] = 0;
+                load_plane<2>(col + (u32)b * (T * 64u), y[b]);
+            }
+            uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+            uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
+#pragma unroll 1
+            for (u32 p = 0; p < k; ++p) {
+                const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+                cl = (cl >> 8) | (ch << 56);
+                ch >>= 8;
+                const uint8_t *nx = col + (p + 1 < k ? p + 1 : p) * (T * ECD_CHUNK);
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    load_plane<2>(nx + (u32)b * (T * 64u), yn[b]);
+                ecgf::mul_xor_jt4(c, acc, y);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+                    y[b][0] = yn[b][0];
+                    y[b][1] = yn[b][1];
+                }
+            }
+            const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
+            if (ost != kNoSlot)
+                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
+            continue;
+        }
 #pragma unroll
         for (int b = 0; b < 8; ++b)
 #pragma unroll

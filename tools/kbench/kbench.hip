@@ -395,9 +395,8 @@ __global__ __launch_bounds__(NW * 64) void kb_combine_db(const CombineArgs a)
  * the dispatch and the body instead of heading every multiply.  The second
  * 16-VGPR input buffer fits the 64-VGPR budget (two 16-wave blocks per CU)
  * only with programs of at most 4 temporaries (gf8_asm_t4.h).  Zero
- * coefficients go through table entry 0 (a no-op body). */
-#include "gf8_asm_t4.h"
-
+ * coefficients go through table entry 0 (a no-op body).  (Now also
+ * ec_combine JT = 4.) */
 template <int K, int NW, bool NTS>
 __global__ __launch_bounds__(NW * 64) void kb_combine_pf(const CombineArgs a)
 {
