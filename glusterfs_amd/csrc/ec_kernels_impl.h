@@ -237,38 +237,11 @@ constexpr u32 gf_pow_c(u32 v, int e)
  * true: acc ^= v^(K-1-j) * x_j, independent products (more ILP, dearer
  * constants). CW: dwords per plane per lane (2: 8 stripes per wave item,
  * 1: 4 stripes, two items per row). */
-/* The 8 planes of one staged input by 8 single ds_read_b64 (256 B per
- * clock per CU) instead of the 4 ds_read2st64_b64 the compiler merges them
- * into (128 B per clock): in asm, with its own wait, so the compiler
- * neither merges them nor knows to wait for them. */
-__device__ __forceinline__ void load_planes_b64(const uint8_t *p, u32 (&d)[8][2])
-{
-    const u32 va = (u32)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
-    v2u q0, q1, q2, q3, q4, q5, q6, q7;
-    asm volatile("ds_read_b64 %0, %8\n"
-                 "ds_read_b64 %1, %8 offset:512\n"
-                 "ds_read_b64 %2, %8 offset:1024\n"
-                 "ds_read_b64 %3, %8 offset:1536\n"
-                 "ds_read_b64 %4, %8 offset:2048\n"
-                 "ds_read_b64 %5, %8 offset:2560\n"
-                 "ds_read_b64 %6, %8 offset:3072\n"
-                 "ds_read_b64 %7, %8 offset:3584\n"
-                 "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "=&v"(q4), "=&v"(q5),
-                   "=&v"(q6), "=&v"(q7)
-                 : "v"(va));
-    d[0][0] = q0[0]; d[0][1] = q0[1]; d[1][0] = q1[0]; d[1][1] = q1[1];
-    d[2][0] = q2[0]; d[2][1] = q2[1]; d[3][0] = q3[0]; d[3][1] = q3[1];
-    d[4][0] = q4[0]; d[4][1] = q4[1]; d[5][0] = q5[0]; d[5][1] = q5[1];
-    d[6][0] = q6[0]; d[6][1] = q6[1]; d[7][0] = q7[0]; d[7][1] = q7[1];
-}
-
-template <int K, int I, bool NTS, bool DIRECT, int CW, bool B64 = false>
+template <int K, int I, bool NTS, bool DIRECT, int CW>
 __device__ __forceinline__ void encode_tile_row(const uint8_t *col, uint8_t *dst)
 {
     constexpr u32 T = 8;
     constexpr u32 v = I + 1;
-    static_assert(!B64 || (CW == 2 && T == 8), "single-b64 reads: 2 dwords per lane, 512-B planes");
     u32 acc[8][CW], y[8][CW];
     if constexpr (DIRECT && v != 1) {
 #pragma unroll
@@ -279,33 +252,21 @@ __device__ __forceinline__ void encode_tile_row(const uint8_t *col, uint8_t *dst
         static_for<0, K>([&](auto J) {
             constexpr int j = decltype(J)::value;
             const uint8_t *src = col + (u32)j * (T * ECD_CHUNK);
-            if constexpr (B64) {
-                load_planes_b64(src, y);
-            } else {
 #pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
-            }
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
             ecgf::mul_xor<gf_pow_c(v, K - 1 - j), CW, true>(acc, acc, y);
         });
     } else {
-        if constexpr (B64) {
-            load_planes_b64(col, acc);
-        } else {
 #pragma unroll
-            for (int b = 0; b < 8; ++b)
-                load_plane<CW>(col + (u32)b * (T * 64u), acc[b]);
-        }
+        for (int b = 0; b < 8; ++b)
+            load_plane<CW>(col + (u32)b * (T * 64u), acc[b]);
 #pragma unroll
         for (int j = 1; j < K; ++j) {
             const uint8_t *src = col + (u32)j * (T * ECD_CHUNK);
-            if constexpr (B64) {
-                load_planes_b64(src, y);
-            } else {
 #pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
-            }
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
             if constexpr (v == 1) {
 #pragma unroll
                 for (int b = 0; b < 8; ++b)
@@ -320,7 +281,7 @@ __device__ __forceinline__ void encode_tile_row(const uint8_t *col, uint8_t *dst
     store_chunk<CW, NTS>(dst, acc);
 }
 
-template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2, bool B64 = false>
+template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2>
 __global__ __launch_bounds__(NW * 64) void ec_encode_tile(const uint8_t *__restrict__ in,
                                                           const FragPtrs out, uint64_t nstripes)
 {
@@ -363,7 +324,7 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile(const uint8_t *__restr
         if (ost < nstripes)
             static_for<0, N>([&](auto I) {
                 if (r == (u32)decltype(I)::value)
-                    encode_tile_row<K, decltype(I)::value, NTS, DIRECT, CW, B64>(col, dst);
+                    encode_tile_row<K, decltype(I)::value, NTS, DIRECT, CW>(col, dst);
             });
     }
 }

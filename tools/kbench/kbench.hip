@@ -570,14 +570,14 @@ static uint8_t kb_gmul(uint8_t a, uint8_t b)
 
 /* Encode through the generic tile kernel (LDS-DMA staging, NT stores):
  * rows = n, coefficient (i+1)^(k-1-j) for input j (ec-method.c:22-36). */
-template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2, bool B64 = false>
+template <int K, int N, int NW, bool NTS, bool DIRECT = false, int CW = 2>
 static void add_encode_tile(std::vector<Variant> &vars, const char *nm, uint64_t nst,
                             const uint8_t *in, const FragPtrs &f)
 {
     const size_t lds = (size_t)K * 8 * ECD_CHUNK;
     const uint64_t g = (nst + 7) / 8;
     vars.push_back({nm, (double)nst * (K + N) * ECD_CHUNK, [=](hipStream_t st) {
-                        hipLaunchKernelGGL((ec_encode_tile<K, N, NW, NTS, DIRECT, CW, B64>), dim3((u32)g),
+                        hipLaunchKernelGGL((ec_encode_tile<K, N, NW, NTS, DIRECT, CW>), dim3((u32)g),
                                            dim3(64 * NW), lds, st, in, f, nst);
                     }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
 }
@@ -838,9 +838,6 @@ int main(int argc, char **argv)
         add_encode_tile<8, 12, 16, true, true>(v, "enc 8+4 vtile NW16 NTS direct", nst, bufA, f);
         add_encode_tile<8, 12, 16, true, false, 1>(v, "enc 8+4 vtile NW16 NTS CW1", nst, bufA, f);
         add_encode_tile<8, 12, 16, true, true, 1>(v, "enc 8+4 vtile NW16 NTS direct CW1", nst, bufA, f);
-        add_encode_tile<8, 12, 16, true, true, 2, true>(v, "enc 8+4 vtile NW16 direct b64", nst, bufA, f);
-        add_encode_tile<8, 12, 12, true, true, 2, true>(v, "enc 8+4 vtile NW12 direct b64", nst, bufA, f);
-        add_encode_tile<8, 12, 12, true, false, 2, true>(v, "enc 8+4 vtile NW12 CW2 b64", nst, bufA, f);
         run_group("encode 8+4", v, rounds, iters, s);
         v.clear();
         {   /* configs[2]: one 64K-stripe batch */
@@ -866,11 +863,8 @@ int main(int argc, char **argv)
         add_encode_tile<16, 20, 16, true, false, 1>(v, "enc 16+4 vtile NW16 NTS CW1", nst, bufA, f);
         add_encode_tile<16, 20, 16, true, true, 1>(v, "enc 16+4 vtile NW16 NTS direct CW1", nst, bufA, f);
         add_encode_tile<16, 20, 16, true, true, 2>(v, "enc 16+4 vtile NW16 NTS direct", nst, bufA, f);
-        /* r02z: single ds_read_b64 per plane (256 B/clk) instead of read2 (128) */
-        add_encode_tile<16, 20, 10, true, false, 2, true>(v, "enc 16+4 vtile NW10 CW2 b64", nst, bufA, f);
-        add_encode_tile<16, 20, 16, true, false, 2, true>(v, "enc 16+4 vtile NW16 CW2 b64", nst, bufA, f);
-        add_encode_tile<16, 20, 20, true, false, 2, true>(v, "enc 16+4 vtile NW20 CW2 b64", nst, bufA, f);
-        add_encode_tile<16, 20, 10, true, true, 2, true>(v, "enc 16+4 vtile NW10 CW2 direct b64", nst, bufA, f);
+        /* r02z: single ds_read_b64 per plane (256 B/clk) instead of read2 (128)
+         * was timed here and retired: kbench_r02z_b64.log, commit 2a288b0 */
         /* r02z: row groups (RB rows per wave item sharing each LDS read) were
          * timed here and retired: kbench_r02z_rb.log, code in commit 822a197 */
         run_group("encode 16+4", v, rounds, iters, s);
