@@ -94,7 +94,8 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
  * JTS / JTM: the multiply dispatch for single / mixed patterns (ec_combine's
  * JT: 0 the compiler's switch, 1 the jump table of ec_gf8_asm.h, 3 the
  * whole-row asm block of ec_gf8_row.h) */
-template <int K, int TS, int NW, int NWM, bool NTS, int JTS, int JTM, bool SL = false>
+template <int K, int TS, int NW, int NWM, bool NTS, int JTS, int JTM, bool SL = false,
+          bool OT = false>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     /* sorted slots: every pattern's run may carry up to 7 padding slots */
@@ -103,7 +104,7 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    const size_t lds = combine_lds<TS>(a.k);
+    const size_t lds = combine_lds<TS>(a.k) + (OT ? combine_lds<TS>(a.rows) : 0);
     if (a.patg) {
         /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
         const void *kern = (const void *)ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM, SL>;
@@ -114,11 +115,11 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
                            dim3((u32)g), dim3(NWM * 64), lds + kPatLdsBytes, s, a);
     }
     else if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, false, true, JTM, SL>),
+        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, false, true, JTM, SL, 1, OT && !SL>),
                            dim3((u32)g), dim3(NWM * 64), lds, s, a);
     else
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS, 2, false, true, JTS>), dim3((u32)g),
-                           dim3(NW * 64), lds, s, a);
+        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS, 2, false, true, JTS, false, 1, OT>),
+                           dim3((u32)g), dim3(NW * 64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -561,6 +562,31 @@ int jt_override()
     return v;
 }
 
+/* Output tile (ec_combine OT) for k <= 4: the rows of a stripe are one
+ * contiguous run of the output (a full decode into stripe-major data) and
+ * the patterns are in the argument segment.  Same box through this
+ * launcher, EC_MI355X_OT alternating, 40 launches after 20
+ * (profiles/ab_ot_r02z.log): 4+2 decode 0.358-0.384 -> 0.346-0.359 ms per
+ * GiB (8 more rounds of 20 launches after 5, profiles/ab_ot42_r02z.log:
+ * median 0.366 -> 0.347), 4+2 mixed 0.361-0.364 -> 0.353-0.358; for k = 8
+ * it loses (1 GiB
+ * decode 0.367-0.379 -> 0.381, 64K-stripe batches 0.092-0.097 -> 0.099),
+ * so k = 8 keeps the register stores.  EC_MI355X_OT=0 turns it off (A/B). */
+bool use_output_tile(const CombineArgs &a)
+{
+    static const bool on = [] {
+        const char *e = getenv("EC_MI355X_OT");
+        return !(e && *e == '0');
+    }();
+    if (!on || a.k > 4 || a.patg || (a.group_pattern && a.group_shift < 3) ||
+        a.out_stride != (uint64_t)a.rows * ECD_CHUNK || ((uintptr_t)a.out_base[0] & 15))
+        return false;
+    for (u32 r = 1; r < a.rows; ++r)
+        if (a.out_base[r] != a.out_base[0] + (size_t)r * ECD_CHUNK)
+            return false;
+    return true;
+}
+
 template <bool NTS>
 int launch_combine_k(hipStream_t s, const CombineArgs &a)
 {
@@ -605,9 +631,11 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
             return launch_combine<8, 1, 16, 16, NTS, 4, 4>(s, a);
         return launch_combine<8, 1, 4, 16, NTS, 4, 4>(s, a);
     }
+    const bool ot = !sw && use_output_tile(a);
     if (a.k <= 4)
         return sw ? launch_combine<4, 1, 8, 8, NTS, 0, 0>(s, a)
-               : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
+               : ot ? launch_combine<4, 1, 8, 8, NTS, 1, 1, false, true>(s, a)
+                    : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
     if (a.k <= 8) {
         /* Full decodes (rows > 4) use 16-wave blocks, single and mixed
          * patterns.  r01 (switch dispatch): 64K-stripe batches 99.5 -> 91 us

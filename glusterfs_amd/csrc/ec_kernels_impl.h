@@ -563,10 +563,18 @@ __device__ __forceinline__ uint64_t slot_stripe(const CombineArgs &a, uint64_t s
  * SLOTS: mixed patterns with groups below a tile (1, 2, 4 stripes): the
  * stripes were sorted by pattern into 8-slot tiles (ec_slots_* kernels), and
  * the block reads its tile's stripes from the slot list. */
+/* OT: the output rows are assembled in LDS after the input tile (stripe s,
+ * row r at (s * rows + r) * 512) and the block writes the tile's stripes as
+ * one contiguous run, 16 B per lane, 1 KiB per wave instruction -- for
+ * outputs laid out stripe-major with out_base[r] = out_base[0] + r * 512 and
+ * out_stride = rows * 512 (full decodes), single or mixed pattern, 8-stripe
+ * tiles, not PG / SLOTS.  Without it each wave stores 64-B plane segments
+ * at a rows*512-B stride straight from its registers. */
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1>
+          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1, bool OT = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
+    static_assert(!OT || (TS == 1 && CW == 2 && !PG && !SLOTS), "output tile: 8-stripe tiles");
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
     /* CW: dwords per plane per lane in the compute phase; a wave item covers
      * SPI = 4*CW stripes of one output row */
@@ -657,9 +665,17 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                     y[b][1] = yn[b][1];
                 }
             }
-            const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
-            if (ost != kNoSlot)
-                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
+            if constexpr (OT) {
+                uint8_t *o = lds + k * (T * ECD_CHUNK) + (s * a.rows + r) * ECD_CHUNK + cc * 8u;
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+            } else {
+                const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
+                if (ost != kNoSlot)
+                    store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW),
+                                         acc);
+            }
             continue;
         }
 #pragma unroll
@@ -689,9 +705,31 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             else
                 ecgf::mul_xor_rt<CW, CSE>(c, acc, y);
         }
-        const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
-        if (ost != kNoSlot)
-            store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
+        if constexpr (OT) {
+            uint8_t *o = lds + k * (T * ECD_CHUNK) + (s * a.rows + r) * ECD_CHUNK + cc * 8u;
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+        } else {
+            const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
+            if (ost != kNoSlot)
+                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
+        }
+    }
+    if constexpr (OT) {
+        __syncthreads();
+        /* the tile's stripes are one contiguous run of the output */
+        const uint8_t *otile = lds + k * (T * ECD_CHUNK);
+        const u32 nst = (u32)(a.nstripes - t0 < T ? a.nstripes - t0 : T);
+        const u32 pieces = nst * a.rows * (ECD_CHUNK / 16);
+        uint8_t *dst = a.out_base[0] + t0 * a.out_stride;
+        for (u32 i = tid; i < pieces; i += NW * 64) {
+            const v4u v = *reinterpret_cast<const v4u *>(otile + i * 16u);
+            if constexpr (NTS)
+                __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(dst + i * 16u));
+            else
+                *reinterpret_cast<v4u *>(dst + i * 16u) = v;
+        }
     }
 }
 

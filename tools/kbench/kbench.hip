@@ -467,6 +467,92 @@ __global__ __launch_bounds__(NW * 64) void kb_combine_pf(const CombineArgs a)
     }
 }
 
+/* Candidate (r02z): decode output assembled in LDS and written as the
+ * tile's contiguous stripe-major run (8 stripes x k chunks, 16 B per lane,
+ * 1 KiB per wave instruction) instead of 64-B plane segments at a k*512-B
+ * stride straight from the registers (PMC: the headline decode writes ~4 %
+ * more HBM bytes than it produces).  Needs out_stride == rows * 512 and
+ * out_base[r] = out + r * 512 (a full decode), single pattern. */
+template <int K, int NW, bool NTS>
+__global__ __launch_bounds__(NW * 64) void kb_combine_ot(const CombineArgs a)
+{
+    constexpr u32 T = 8;
+    constexpr u32 NI = K * T * 32 / 64;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    uint8_t *otile = lds + k * (T * ECD_CHUNK);      /* [stripe][row][512 B] */
+    const PatWords<false> pw(a, 0u, lane, nullptr);
+#pragma unroll
+    for (u32 j = 0; j < (NI + NW - 1) / NW; ++j) {
+        const u32 ins = j * NW + wave;
+        if (ins >= NI)
+            break;
+        const u32 p = ins / (T / 2);
+        if (p >= k)
+            break;
+        const u32 el = (ins * 64 + lane) % (T * 32);
+        const u32 s = (el >> 2) % T;
+        const uint64_t st = t0 + s;
+        if (st < a.nstripes) {
+            const uint8_t *g = a.in_base[pw.byte(a, p)] + st * a.in_stride +
+                               ((el >> 2) / T) * 64u + (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+        }
+    }
+    __syncthreads();
+    const u32 cs = lane >> 3, cc = lane & 7u;
+    const u32 rows = a.rows;
+    for (u32 r = wave; r < rows; r += NW) {
+        const uint8_t *col = lds + cs * 64u + cc * 8u;
+        const u32 rw = a.kw * (1 + r);
+        const u32 w0 = pw.word(a, rw);
+        const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+        const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
+        const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
+        u32 acc[8][2], y[8][2];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc[b][0] = acc[b][1] = 0;
+        uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
+#pragma unroll 1
+        for (u32 p = 0; p < k; ++p) {
+            const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+            cl = (cl >> 8) | (ch << 56);
+            ch >>= 8;
+            if (c == 0)
+                continue;
+            const uint8_t *src = col + p * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<2>(src + (u32)b * (T * 64u), y[b]);
+            ecgf::mul_xor_jt<2>(c, acc, y);
+        }
+        uint8_t *o = otile + (cs * rows + r) * ECD_CHUNK + cc * 8u;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+    }
+    __syncthreads();
+    /* the tile's 8 stripes are one contiguous run of the output */
+    const uint64_t nst = a.nstripes - t0 < T ? a.nstripes - t0 : T;
+    const u32 pieces = (u32)nst * rows * (ECD_CHUNK / 16);
+    uint8_t *dst = a.out_base[0] + t0 * a.out_stride;
+    for (u32 i = tid; i < pieces; i += NW * 64) {
+        const v4u v = *reinterpret_cast<const v4u *>(otile + i * 16u);
+        if constexpr (NTS)
+            __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(dst + i * 16u));
+        else
+            *reinterpret_cast<v4u *>(dst + i * 16u) = v;
+    }
+}
+
 /* decode k+r with the first r bricks missing, coefficients from the host
  * inverse (a dense k x k matrix is all we need for timing; correctness of
  * the math is covered by the parity tests -- here variants are compared
@@ -515,6 +601,19 @@ static void add_decode(std::vector<Variant> &vars, uint64_t nst, uint8_t *const 
     add("TS1 NW4 NTS jt", ec_combine<K, 1, 4, false, true, 2, false, true, 1>, 1, 4);
     add("TS1 NW8 NTS jt", ec_combine<K, 1, 8, false, true, 2, false, true, 1>, 1, 8);
     add("TS1 NW16 NTS jt", ec_combine<K, 1, 16, false, true, 2, false, true, 1>, 1, 16);
+    /* r02z: output assembled in LDS, written as one contiguous run */
+    auto addot = [&](const char *nm, auto kern, int nw) {
+        const size_t lds = 2 * (size_t)K * 8 * ECD_CHUNK;
+        CHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+        const uint64_t g = (nst + 7) / 8;
+        vars.push_back({nm, bytes, [=](hipStream_t s) {
+                            hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * nw), lds, s, a);
+                        }, out, ob});
+    };
+    addot("TS1 NW8 NTS ot", kb_combine_ot<K, 8, true>, 8);
+    addot("TS1 NW16 NTS ot", kb_combine_ot<K, 16, true>, 16);
+    addot("TS1 NW8 ot (default stores)", kb_combine_ot<K, 8, false>, 8);
     /* r02z: next input's LDS reads issued before the current multiply */
     add("TS1 NW8 NTS pf", kb_combine_pf<K, 8, true>, 1, 8);
     add("TS1 NW16 NTS pf", kb_combine_pf<K, 16, true>, 1, 16);
