@@ -674,7 +674,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": "ec_combine<K=4,TS=1,NW=8,NTS,JT> (decode, jump-table multiply)",
+            "kernel": "ec_combine<K=4,TS=1,NW=8,NTS,JT,OT=1> (decode, jump-table multiply, output tile)",
             "algorithmic_bytes_per_launch": 2 * r["user"],
             "avg_launch_ms": round(kt * 1e3, 4),
         },

@@ -95,7 +95,7 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
  * JT: 0 the compiler's switch, 1 the jump table of ec_gf8_asm.h, 3 the
  * whole-row asm block of ec_gf8_row.h) */
 template <int K, int TS, int NW, int NWM, bool NTS, int JTS, int JTM, bool SL = false,
-          bool OT = false>
+          int OT = 0>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     /* sorted slots: every pattern's run may carry up to 7 padding slots */
@@ -115,7 +115,7 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
                            dim3((u32)g), dim3(NWM * 64), lds + kPatLdsBytes, s, a);
     }
     else if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, false, true, JTM, SL, 1, OT && !SL>),
+        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, false, true, JTM, SL, 1, SL ? 0 : OT>),
                            dim3((u32)g), dim3(NWM * 64), lds, s, a);
     else
         hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS, 2, false, true, JTS, false, 1, OT>),
@@ -162,6 +162,8 @@ int launch_encode_tile(hipStream_t s, uint64_t nstripes, const void *in, void *c
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+int output_tile_mode(const CombineArgs &a);
+
 /* 4+2: the encode matrix (row i: (i+1)^(3-j), ec-method.c:22-36) as one
  * ec_combine pattern over the stripe-major input */
 int launch_encode_42_combine(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
@@ -193,7 +195,8 @@ int launch_encode_42_combine(hipStream_t s, uint64_t nstripes, const void *in, v
     const int rc = ecdk_pack_args(&c, &a);
     if (rc)
         return rc;
-    return launch_combine<4, 1, 16, 16, true, 1, 1>(s, a);
+    return output_tile_mode(a) == 2 ? launch_combine<4, 1, 16, 16, true, 1, 1, false, 2>(s, a)
+                                    : launch_combine<4, 1, 16, 16, true, 1, 1>(s, a);
 }
 
 } // namespace
@@ -572,19 +575,27 @@ int jt_override()
  * it loses (1 GiB
  * decode 0.367-0.379 -> 0.381, 64K-stripe batches 0.092-0.097 -> 0.099),
  * so k = 8 keeps the register stores.  EC_MI355X_OT=0 turns it off (A/B). */
-bool use_output_tile(const CombineArgs &a)
+/* 0: no output tile; 1: stripe-major run (full decode); 2: fragment rows
+ * (out_stride = 512, EC_MI355X_OT=2 only: A/B) */
+int output_tile_mode(const CombineArgs &a)
 {
-    static const bool on = [] {
+    static const int mode = [] {
         const char *e = getenv("EC_MI355X_OT");
-        return !(e && *e == '0');
+        return e && (*e == '0' || *e == '2') ? *e - '0' : 1;
     }();
-    if (!on || a.k > 4 || a.patg || (a.group_pattern && a.group_shift < 3) ||
-        a.out_stride != (uint64_t)a.rows * ECD_CHUNK || ((uintptr_t)a.out_base[0] & 15))
-        return false;
+    if (mode == 0 || a.k > 4 || a.patg || (a.group_pattern && a.group_shift < 3))
+        return 0;
+    for (u32 r = 0; r < a.rows; ++r)
+        if ((uintptr_t)a.out_base[r] & 15)
+            return 0;
+    if (mode == 2 && a.out_stride == ECD_CHUNK)
+        return 2;
+    if (a.out_stride != (uint64_t)a.rows * ECD_CHUNK)
+        return 0;
     for (u32 r = 1; r < a.rows; ++r)
         if (a.out_base[r] != a.out_base[0] + (size_t)r * ECD_CHUNK)
-            return false;
-    return true;
+            return 0;
+    return 1;
 }
 
 template <bool NTS>
@@ -631,11 +642,12 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
             return launch_combine<8, 1, 16, 16, NTS, 4, 4>(s, a);
         return launch_combine<8, 1, 4, 16, NTS, 4, 4>(s, a);
     }
-    const bool ot = !sw && use_output_tile(a);
+    const int ot = sw ? 0 : output_tile_mode(a);
     if (a.k <= 4)
-        return sw ? launch_combine<4, 1, 8, 8, NTS, 0, 0>(s, a)
-               : ot ? launch_combine<4, 1, 8, 8, NTS, 1, 1, false, true>(s, a)
-                    : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
+        return sw        ? launch_combine<4, 1, 8, 8, NTS, 0, 0>(s, a)
+               : ot == 1 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, false, 1>(s, a)
+               : ot == 2 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, false, 2>(s, a)
+                         : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
     if (a.k <= 8) {
         /* Full decodes (rows > 4) use 16-wave blocks, single and mixed
          * patterns.  r01 (switch dispatch): 64K-stripe batches 99.5 -> 91 us

@@ -563,15 +563,16 @@ __device__ __forceinline__ uint64_t slot_stripe(const CombineArgs &a, uint64_t s
  * SLOTS: mixed patterns with groups below a tile (1, 2, 4 stripes): the
  * stripes were sorted by pattern into 8-slot tiles (ec_slots_* kernels), and
  * the block reads its tile's stripes from the slot list. */
-/* OT: the output rows are assembled in LDS after the input tile (stripe s,
- * row r at (s * rows + r) * 512) and the block writes the tile's stripes as
- * one contiguous run, 16 B per lane, 1 KiB per wave instruction -- for
- * outputs laid out stripe-major with out_base[r] = out_base[0] + r * 512 and
- * out_stride = rows * 512 (full decodes), single or mixed pattern, 8-stripe
- * tiles, not PG / SLOTS.  Without it each wave stores 64-B plane segments
- * at a rows*512-B stride straight from its registers. */
+/* OT: the output rows are assembled in LDS after the input tile and the
+ * block writes them in destination order, 16 B per lane, 1 KiB per wave
+ * instruction, instead of each wave storing 64-B plane segments at a
+ * stride straight from its registers.  OT = 1: stripe-major outputs
+ * (out_base[r] = out_base[0] + r * 512, out_stride = rows * 512: full
+ * decodes), stripe s / row r at (s * rows + r) * 512, the tile one run;
+ * OT = 2: fragment outputs (out_stride = 512: encode, heal), row r / stripe
+ * s at (r * 8 + s) * 512, one run per row.  8-stripe tiles, not PG / SLOTS. */
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1, bool OT = false>
+          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1, int OT = 0>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     static_assert(!OT || (TS == 1 && CW == 2 && !PG && !SLOTS), "output tile: 8-stripe tiles");
@@ -666,7 +667,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                 }
             }
             if constexpr (OT) {
-                uint8_t *o = lds + k * (T * ECD_CHUNK) + (s * a.rows + r) * ECD_CHUNK + cc * 8u;
+                uint8_t *o = lds + k * (T * ECD_CHUNK) + (OT == 1 ? s * a.rows + r : r * T + s) * ECD_CHUNK + cc * 8u;
 #pragma unroll
                 for (int b = 0; b < 8; ++b)
                     *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
@@ -706,7 +707,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                 ecgf::mul_xor_rt<CW, CSE>(c, acc, y);
         }
         if constexpr (OT) {
-            uint8_t *o = lds + k * (T * ECD_CHUNK) + (s * a.rows + r) * ECD_CHUNK + cc * 8u;
+            uint8_t *o = lds + k * (T * ECD_CHUNK) + (OT == 1 ? s * a.rows + r : r * T + s) * ECD_CHUNK + cc * 8u;
 #pragma unroll
             for (int b = 0; b < 8; ++b)
                 *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
@@ -721,14 +722,24 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         /* the tile's stripes are one contiguous run of the output */
         const uint8_t *otile = lds + k * (T * ECD_CHUNK);
         const u32 nst = (u32)(a.nstripes - t0 < T ? a.nstripes - t0 : T);
-        const u32 pieces = nst * a.rows * (ECD_CHUNK / 16);
-        uint8_t *dst = a.out_base[0] + t0 * a.out_stride;
+        const u32 per_row = nst * (ECD_CHUNK / 16);     /* 16-B pieces of one row */
+        const u32 pieces = per_row * a.rows;
         for (u32 i = tid; i < pieces; i += NW * 64) {
-            const v4u v = *reinterpret_cast<const v4u *>(otile + i * 16u);
+            const uint8_t *src;
+            uint8_t *dst;
+            if constexpr (OT == 1) {
+                src = otile + i * 16u;
+                dst = a.out_base[0] + t0 * a.out_stride + i * 16u;
+            } else {
+                const u32 r = i / per_row, w = i % per_row;
+                src = otile + (r * T) * ECD_CHUNK + w * 16u;
+                dst = a.out_base[r] + t0 * ECD_CHUNK + w * 16u;
+            }
+            const v4u v = *reinterpret_cast<const v4u *>(src);
             if constexpr (NTS)
-                __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(dst + i * 16u));
+                __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(dst));
             else
-                *reinterpret_cast<v4u *>(dst + i * 16u) = v;
+                *reinterpret_cast<v4u *>(dst) = v;
         }
     }
 }
