@@ -576,14 +576,16 @@ int jt_override()
  * decode 0.367-0.379 -> 0.381, 64K-stripe batches 0.092-0.097 -> 0.099),
  * so k = 8 keeps the register stores.  EC_MI355X_OT=0 turns it off (A/B). */
 /* 0: no output tile; 1: stripe-major run (full decode); 2: fragment rows
- * (out_stride = 512, EC_MI355X_OT=2 only: A/B) */
+ * (out_stride = 512, EC_MI355X_OT=2 only: A/B); EC_MI355X_OT=3: stripe-major
+ * runs for k <= 8 too (A/B) */
 int output_tile_mode(const CombineArgs &a)
 {
     static const int mode = [] {
         const char *e = getenv("EC_MI355X_OT");
-        return e && (*e == '0' || *e == '2') ? *e - '0' : 1;
+        return e && (*e == '0' || *e == '2' || *e == '3') ? *e - '0' : 1;
     }();
-    if (mode == 0 || a.k > 4 || a.patg || (a.group_pattern && a.group_shift < 3))
+    if (mode == 0 || a.k > (mode == 3 ? 8u : 4u) || a.patg ||
+        (a.group_pattern && a.group_shift < 3))
         return 0;
     for (u32 r = 0; r < a.rows; ++r)
         if ((uintptr_t)a.out_base[r] & 15)
@@ -648,6 +650,8 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
                : ot == 1 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, false, 1>(s, a)
                : ot == 2 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, false, 2>(s, a)
                          : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
+    if (a.k <= 8 && ot == 1 && a.rows > 4)         /* EC_MI355X_OT=3 (A/B) */
+        return launch_combine<8, 1, 16, 16, NTS, 1, 1, false, 1>(s, a);
     if (a.k <= 8) {
         /* Full decodes (rows > 4) use 16-wave blocks, single and mixed
          * patterns.  r01 (switch dispatch): 64K-stripe batches 99.5 -> 91 us
