@@ -104,7 +104,7 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    const size_t lds = combine_lds<TS>(a.k) + (OT ? combine_lds<TS>(a.rows) : 0);
+    const size_t lds = combine_lds<TS>(a.k) + (OT && OT != 4 ? combine_lds<TS>(a.rows) : 0);
     if (a.patg) {
         /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
         const void *kern = (const void *)ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM, SL>;
@@ -580,10 +580,20 @@ int jt_override()
  * runs for k <= 8 too (A/B) */
 int output_tile_mode(const CombineArgs &a)
 {
-    static const int mode = [] {
+    static const int mode0 = [] {
         const char *e = getenv("EC_MI355X_OT");
-        return e && (*e == '0' || *e == '2' || *e == '3') ? *e - '0' : 1;
+        return e && (*e == '0' || *e == '2' || *e == '3' || *e == '4') ? *e - '0' : 1;
     }();
+    int mode = mode0;
+    if (mode == 4 && a.k > 8 && !a.patg && !a.group_pattern && a.rows <= a.k &&
+        a.out_stride == (uint64_t)a.rows * ECD_CHUNK && !((uintptr_t)a.out_base[0] & 15)) {
+        for (u32 r = 1; r < a.rows; ++r)
+            if (a.out_base[r] != a.out_base[0] + (size_t)r * ECD_CHUNK)
+                return 0;
+        return 4;                 /* k = 16 in-place output tile (A/B) */
+    }
+    if (mode == 4)
+        mode = 1;
     if (mode == 0 || a.k > (mode == 3 ? 8u : 4u) || a.patg ||
         (a.group_pattern && a.group_shift < 3))
         return 0;
@@ -668,6 +678,8 @@ int launch_combine_k(hipStream_t s, const CombineArgs &a)
         return sw ? launch_combine<8, 1, 4, 8, NTS, 0, 0>(s, a)
                   : launch_combine<8, 1, 4, 16, NTS, 1, 1>(s, a);
     }
+    if (ot == 4)                                /* EC_MI355X_OT=4 (A/B) */
+        return launch_combine<16, 1, 16, 16, NTS, 1, 1, false, 4>(s, a);
     return sw ? launch_combine<16, 1, 16, 16, NTS, 0, 0>(s, a)
            : launch_combine<16, 1, 16, 16, NTS, 1, 1>(s, a);
 }

@@ -627,6 +627,60 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     /* compute: (row, 8-stripe subtile) items spread over the NW waves */
     const u32 cs = lane / LPS, cc = lane % LPS;
     const u32 items = a.rows * IPT;
+    if constexpr (OT == 4) {
+        /* OT = 4: the output tile of OT = 1 assembled in place of the input
+         * tile once every wave is done reading it (no extra LDS; needs one
+         * item per wave: rows <= NW, checked by the launcher) */
+        static_assert(JT == 1 && CW == 2 && TS == 1, "in-place output tile: jump table, CW 2");
+        u32 acc[8][2], y[8][2];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc[b][0] = acc[b][1] = 0;
+        const bool has = wave < items;
+        const u32 r = has ? wave : 0u;
+        if (has) {
+            const uint8_t *col = lds + cs * 64u + cc * 8u;
+            const u32 rw = a.kw * (1 + r);
+            const u32 w0 = pw.word(a, rw);
+            const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+            const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
+            const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
+            uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+            uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
+#pragma unroll 1
+            for (u32 p = 0; p < k; ++p) {
+                const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+                cl = (cl >> 8) | (ch << 56);
+                ch >>= 8;
+                if (c == 0)                  /* ec-code-c.c:11666-11676 */
+                    continue;
+                const uint8_t *src = col + p * (T * ECD_CHUNK);
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    load_plane<2>(src + (u32)b * (T * 64u), y[b]);
+                ecgf::mul_xor_jt<2>(c, acc, y);
+            }
+        }
+        __syncthreads();                     /* the input tile is free */
+        if (has) {
+            uint8_t *o = lds + (cs * a.rows + r) * ECD_CHUNK + cc * 8u;
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+        }
+        __syncthreads();
+        const u32 nst = (u32)(a.nstripes - t0 < T ? a.nstripes - t0 : T);
+        const u32 pieces = nst * a.rows * (ECD_CHUNK / 16);
+        uint8_t *dst = a.out_base[0] + t0 * a.out_stride;
+        for (u32 i = tid; i < pieces; i += NW * 64) {
+            const v4u v = *reinterpret_cast<const v4u *>(lds + i * 16u);
+            if constexpr (NTS)
+                __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(dst + i * 16u));
+            else
+                *reinterpret_cast<v4u *>(dst + i * 16u) = v;
+        }
+        return;
+    }
     for (u32 it = wave; it < items; it += NW) {
         const u32 r = it / IPT, s = (it % IPT) * SPI + cs;
         const uint8_t *col = lds + s * 64u + cc * (4u * CW);
