@@ -1,0 +1,86 @@
+"""GPU parity of the A/B instantiations.
+
+The tuning knobs (INTEGRATION.md "A/B knobs", read once per process by
+ec_kernels.hip) select kernel instantiations the default run never launches:
+the k = 8 / k = 16 output tiles, fragment-output tiles, the compiler-switch
+and software-pipelined multiplies, the other encoders, other wave counts,
+default-policy stores, the uncached pattern table.  Each runs here in its own
+process through the C ABI, bit-exact against the oracle on device-resident
+encode, full / partial decode (ragged tiles included) and mixed decode.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r"""
+import itertools, sys
+sys.path.insert(0, "oracle")
+import numpy as np, torch
+import glusterfs_amd as g
+import oracle as O           # the checker
+
+rng = np.random.default_rng(7)
+def rb(n):
+    return rng.integers(0, 256, n, dtype=np.uint8)
+def dev(a):
+    return torch.from_numpy(a).cuda()
+
+for k, n in ((4, 6), (8, 12), (16, 20)):
+    allm = [sum(1 << b for b in c) for c in itertools.combinations(range(n), k)]
+    pick = np.random.default_rng(k).choice(len(allm), min(24, len(allm)), replace=False)
+    masks = [allm[i] for i in sorted(pick)]
+    with g.ECMatrixList(k, n) as L:
+        for nst in (13, 77, 1031):
+            data = rb(512 * k * nst)
+            want = O.encode(k, n, data)
+            outs = [torch.empty(512 * nst, dtype=torch.uint8, device="cuda") for _ in range(n)]
+            L.encode_batch(nst, dev(data), outs)
+            for i in range(n):
+                assert np.array_equal(outs[i].cpu().numpy(), want[i]), ("enc", k, n, nst, i)
+            frags = [rb(512 * nst) for _ in range(n)]
+            dfr = [dev(f) for f in frags]
+            out = torch.empty(512 * k * nst, dtype=torch.uint8, device="cuda")
+            for m in masks:
+                rows = O.mask_rows(m)
+                out.fill_(0xA5)
+                L.decode_batch(nst, m, rows, [dfr[r - 1] for r in rows], out)
+                exp = O.decode(k, rows, [frags[r - 1] for r in rows])
+                assert np.array_equal(out.cpu().numpy(), exp), ("dec", k, n, nst, hex(m))
+        group, ng = 16, 12
+        nst = group * ng
+        frags = [rb(512 * nst) for _ in range(n)]
+        ms = masks[:6]
+        ids = rng.integers(0, len(ms), ng).astype(np.uint8)
+        out = torch.empty(512 * k * nst, dtype=torch.uint8, device="cuda")
+        L.decode_mixed_device(0, None, nst, group, dev(ids), ms, [dev(f) for f in frags], out)
+        g.sync_device(0)
+        got = out.cpu().numpy()
+        span = 512 * group
+        for gi in range(ng):
+            rows = O.mask_rows(ms[ids[gi]])
+            exp = O.decode(k, rows, [frags[r - 1][gi * span:(gi + 1) * span] for r in rows])
+            assert np.array_equal(got[gi * span * k:(gi + 1) * span * k], exp), ("mixed", k, gi)
+print("ok")
+"""
+
+KNOBS = [
+    ("EC_MI355X_OT", "0"), ("EC_MI355X_OT", "2"), ("EC_MI355X_OT", "3"), ("EC_MI355X_OT", "4"),
+    ("EC_MI355X_JT", "0"), ("EC_MI355X_JT", "4"), ("EC_MI355X_ENC", "0"), ("EC_MI355X_ENC", "2"),
+    ("EC_MI355X_NW4", "16"), ("EC_MI355X_NW8", "8"), ("EC_MI355X_NW16", "8"), ("EC_MI355X_NTS", "0"),
+    ("EC_MI355X_PATCACHE", "0"),
+]
+
+
+@pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])
+def test_ab_instantiation_bit_exact(knob, value):
+    env = dict(os.environ, EC_MI355X_QUIET="1")
+    env[knob] = value
+    r = subprocess.run([sys.executable, "-c", SCRIPT], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
