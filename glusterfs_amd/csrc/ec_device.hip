@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -115,6 +116,9 @@ void host_devices_from_env()
 /* EC_MI355X_DEBUG=1: count the HIP pointer queries of the host-call checks
  * and print them at exit (development probe for the routing cost). */
 std::atomic<uint64_t> g_ptr_queries{0}, g_map_queries{0};
+/* Generation of the library's own host-memory frees: invalidates the
+ * per-thread host-page cache of ecd_ptr_device (below). */
+std::atomic<uint32_t> g_host_gen{0};
 
 void print_query_counts()
 {
@@ -373,6 +377,7 @@ int grow(uint8_t *(&slot)[kSlots], size_t &cap, size_t want)
         if (p) {
             (void)hipHostFree(p);
             p = nullptr;
+            g_host_gen.fetch_add(1, std::memory_order_release);
         }
     cap = 0;
     for (auto &p : slot)
@@ -997,10 +1002,41 @@ void ecd_inject_faults(uint32_t n)
  * runtime does not know at all (pageable malloc / mmap memory: the query
  * reports hipMemoryTypeUnregistered, or fails) are cached.  Memory the
  * runtime allocated -- device buffers, and pinned host buffers, which come
- * from the same GPU virtual range -- is queried every time: once freed, its addresses are handed out again, and a
- * pinned page cached as "host" came back as a torch device tensor in the GPU
- * tests (-EINVAL on a device-resident encode). */
-static thread_local uintptr_t t_host_page[256];
+ * from the same GPU virtual range -- is queried every time: once freed, its
+ * addresses are handed out again, and a pinned page cached as "host" came
+ * back as a torch device tensor in the GPU tests (-EINVAL on a
+ * device-resident encode).
+ * An entry also expires: a pageable buffer can be unmapped and its range
+ * handed to a later device allocation (the thunk maps GPU virtual memory
+ * with mmap too), and a stale "host" verdict would send device memory down
+ * the CPU path.  So every entry carries the time it was made (coarse
+ * monotonic clock, vDSO: ~20 ns) and the generation of the library's own
+ * frees (ecd_host_free / unregister / staging growth bump g_host_gen); it
+ * is trusted for EC_HOSTPAGE_MS (default 20 ms) -- at most ~50 queries per
+ * second per page and thread, against one per call without the cache. */
+struct HostPage {
+    uintptr_t pg;        /* page number + 1; 0 = empty */
+    uint64_t until_ns;
+    uint32_t gen;
+};
+static thread_local HostPage t_host_page[256];
+
+static uint64_t hostpage_ttl_ns()
+{
+    static const uint64_t v = [] {
+        const char *e = getenv("EC_HOSTPAGE_MS");
+        const long ms = e ? atol(e) : 20;
+        return (uint64_t)(ms >= 0 && ms <= 10000 ? ms : 20) * 1000000ull;
+    }();
+    return v;
+}
+
+static uint64_t coarse_ns()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC_COARSE, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 
 int ecd_ptr_device(const void *p)
 {
@@ -1010,19 +1046,22 @@ int ecd_ptr_device(const void *p)
     /* Fibonacci hashing: iobufs sit at regular page strides (65 pages for
      * 256 KiB mmap'ed buffers), which a xor-fold of the page number mapped
      * onto a few slots (~4 misses per decode call, 16 threads) */
-    uintptr_t &slot = t_host_page[(uint64_t)(pg * 0x9E3779B97F4A7C15ull) >> 56];
-    if (slot == pg + 1)
+    HostPage &slot = t_host_page[(uint64_t)(pg * 0x9E3779B97F4A7C15ull) >> 56];
+    const uint32_t gen = g_host_gen.load(std::memory_order_acquire);
+    const uint64_t now = hostpage_ttl_ns() ? coarse_ns() : 0;
+    if (slot.pg == pg + 1 && slot.gen == gen && now < slot.until_ns)
         return -1;
     hipPointerAttribute_t a;
     g_ptr_queries.fetch_add(1, std::memory_order_relaxed);
+    const HostPage fresh = {pg + 1, now + hostpage_ttl_ns(), gen};
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
-        slot = pg + 1;
+        slot = fresh;
         return -1;
     }
     if (a.type != hipMemoryTypeDevice) {
         if (a.type == hipMemoryTypeUnregistered)
-            slot = pg + 1;
+            slot = fresh;
         return -1;
     }
     for (int i = 0; i < g_ndev; ++i)
@@ -1043,8 +1082,10 @@ void *ecd_host_alloc(size_t bytes)
 
 void ecd_host_free(void *p)
 {
-    if (p)
+    if (p) {
         (void)hipHostFree(p);
+        g_host_gen.fetch_add(1, std::memory_order_release);
+    }
 }
 
 int ecd_host_register(void *p, size_t bytes)
@@ -1066,6 +1107,7 @@ int ecd_host_unregister(void *p)
     if (ecd_device_count() == 0)
         return -ENODEV;
     const hipError_t e = hipHostUnregister(p);
+    g_host_gen.fetch_add(1, std::memory_order_release);
     if (e != hipSuccess) {
         set_err("hipHostUnregister", e);
         return -EINVAL;

@@ -34,12 +34,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <vector>
 
 #include <cstddef>
 #include <cstring>
-#include <mutex>
 
 #include "ec_kernels.h"
 #include "ec_kernels_impl.h"
@@ -216,7 +216,10 @@ static int enc_mode()
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                        const void *in, void *const *out, bool zc)
 {
-    const bool tiles = !zc && enc_mode() != 0;
+    /* the tile encoders stage their input by LDS-DMA in 16-byte pieces; an
+     * input at any other alignment (a tensor slice) keeps the
+     * register-resident encoder, whose loads take any byte address */
+    const bool tiles = !zc && enc_mode() != 0 && !((uintptr_t)in & 15);
     if (tiles && k == 4 && n == 6)
         return launch_encode_42_combine(s, nstripes, in, out);
     if (tiles && k == 8 && n == 12 && (nstripes > (1u << 17) || enc_mode() == 2))
@@ -340,7 +343,11 @@ int enqueue_upload(hipStream_t s, const std::vector<u32> &w, u32 *tab)
  * device (per device, LRU): a repeated call skips the allocation and the
  * upload launches (one per 2 KiB: ~9 for 64 masks of 16+4, ~50 us of
  * stream time per call).  An entry is reused only for identical words, and
- * evicted (LRU, after the device drains) only when no call holds it. */
+ * evicted (LRU) only when no call holds it.  Every stream that launched a
+ * reader records the entry's event for that stream at release(); eviction
+ * waits on those events with the cache lock dropped (the slot is marked
+ * busy meanwhile), so one caller's eviction never blocks other callers or
+ * waits for unrelated work on the device. */
 class PatTableCache {
   public:
     struct Ref {
@@ -364,7 +371,7 @@ class PatTableCache {
         uint64_t h = 1469598103934665603ull;     /* FNV-1a over the words */
         for (u32 x : w)
             h = (h ^ x) * 1099511628211ull;
-        std::lock_guard<std::mutex> g(mu_);
+        std::unique_lock<std::mutex> g(mu_);
         int victim = -1;
         for (int i = 0; i < kEntries; ++i) {
             Entry &e = e_[i];
@@ -382,19 +389,32 @@ class PatTableCache {
         if (victim < 0)
             return -EBUSY;                    /* every entry in use: per call */
         Entry &e = e_[victim];
+        e.inflight = 1;                       /* ours: nobody else picks it */
+        e.hash = 0;
+        e.words.clear();
         if (e.ptr) {
-            /* evict: its readers may sit on several callers' streams, so
-             * wait for the whole device (rare: > kEntries live mask sets) */
-            (void)hipDeviceSynchronize();
-            (void)hipFree(e.ptr);
+            /* evict: wait for the streams that read it, without the lock */
+            std::vector<hipEvent_t> wait;
+            for (auto &r : e.readers)
+                wait.push_back(r.second);
+            u32 *old = e.ptr;
             e.ptr = nullptr;
+            g.unlock();
+            for (hipEvent_t ev : wait)
+                (void)hipEventSynchronize(ev);
+            (void)hipFree(old);
+            g.lock();
         }
         if (e.dev != dev) {
+            for (auto &r : e.readers)
+                (void)hipEventDestroy(r.second);
+            e.readers.clear();
             if (e.ready)
                 (void)hipEventDestroy(e.ready);
             e.ready = nullptr;
             if (hipEventCreateWithFlags(&e.ready, hipEventDisableTiming) != hipSuccess) {
                 (void)hipGetLastError();
+                e.inflight = 0;
                 return -EIO;
             }
             e.dev = dev;
@@ -402,28 +422,53 @@ class PatTableCache {
         if (hipMalloc(reinterpret_cast<void **>(&e.ptr), w.size() * 4) != hipSuccess) {
             (void)hipGetLastError();
             e.ptr = nullptr;
+            e.inflight = 0;
             return -ENOMEM;
         }
         if (enqueue_upload(s, w, e.ptr) != 0 || hipEventRecord(e.ready, s) != hipSuccess) {
             (void)hipStreamSynchronize(s);
             (void)hipFree(e.ptr);
             e.ptr = nullptr;
+            e.inflight = 0;
             return -EIO;
         }
         e.hash = h;
         e.words = w;
-        e.inflight = 1;
         e.tick = ++tick_;
         ref.slot = victim;
         ref.ptr = e.ptr;
         return 0;
     }
 
-    /* The work that reads the table has been enqueued. */
-    void release(const Ref &ref)
+    /* The work that reads the table has been enqueued on `s`. */
+    void release(const Ref &ref, hipStream_t s)
     {
         std::lock_guard<std::mutex> g(mu_);
-        --e_[ref.slot].inflight;
+        Entry &e = e_[ref.slot];
+        hipEvent_t ev = nullptr;
+        for (auto &r : e.readers)
+            if (r.first == s)
+                ev = r.second;
+        if (!ev) {
+            if (e.readers.size() >= kMaxReaders) {
+                /* many distinct streams: fold the oldest reader into a wait
+                 * now (rare; keeps the list bounded) */
+                (void)hipEventSynchronize(e.readers.front().second);
+                (void)hipEventDestroy(e.readers.front().second);
+                e.readers.erase(e.readers.begin());
+            }
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess)
+                e.readers.emplace_back(s, ev);
+            else {
+                (void)hipGetLastError();
+                ev = nullptr;
+            }
+        }
+        if (!ev || hipEventRecord(ev, s) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(s);  /* cannot track it: drain it */
+        }
+        --e.inflight;
     }
 
   private:
@@ -433,9 +478,11 @@ class PatTableCache {
         std::vector<u32> words;
         u32 *ptr = nullptr;
         hipEvent_t ready = nullptr;           /* the upload has landed */
+        std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
         int inflight = 0;
     };
     static constexpr int kEntries = 16;
+    static constexpr size_t kMaxReaders = 16;
     std::mutex mu_;
     Entry e_[kEntries];
     uint64_t tick_ = 0;
@@ -697,7 +744,7 @@ int combine_any(hipStream_t s, const ecd_combine_desc_t *d)
     if (rc == 0)
         rc = launch_combine_k<NTS>(s, a);
     if (ref.slot >= 0)
-        pat_tables().release(ref);
+        pat_tables().release(ref, s);
     if (tab)
         (void)hipFreeAsync(tab, s);
     return rc;
@@ -741,6 +788,80 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
     return 0;
 }
 
+namespace {
+
+bool inputs_misaligned(const ecd_combine_desc_t *d)
+{
+    for (u32 p = 0; p < ECD_MAX_ROWS; ++p)
+        if (d->in_base[p] && ((uintptr_t)d->in_base[p] & 15))
+            return true;
+    return false;
+}
+
+/* Every combine stages its inputs by LDS-DMA (global_load_lds_dwordx4),
+ * 16 bytes per lane: inputs at another alignment (e.g. torch slices at an
+ * odd offset) are first copied, stream-ordered, to aligned scratch -- one
+ * copy for bases that share a buffer (the stripe-major input of an encode:
+ * in_base[p] = in + p * 512), one per base otherwise. */
+template <bool NTS>
+int combine_realigned(hipStream_t s, const ecd_combine_desc_t *d)
+{
+    if (d->in_stride & 15)
+        return -EINVAL;
+    std::unique_ptr<ecd_combine_desc_t> c(new ecd_combine_desc_t(*d));
+    const uint64_t span = d->nstripes ? (d->nstripes - 1) * d->in_stride + ECD_CHUNK : 0;
+    uintptr_t lo = UINTPTR_MAX, hi = 0, mis = 16;
+    uint64_t total = 0;
+    bool same = true;
+    for (u32 p = 0; p < ECD_MAX_ROWS; ++p) {
+        const uintptr_t b = (uintptr_t)d->in_base[p];
+        if (!b || !(b & 15))
+            continue;
+        same &= mis == 16 || mis == (b & 15);
+        mis = b & 15;
+        lo = std::min(lo, b);
+        hi = std::max<uintptr_t>(hi, b + span);
+        total += span;
+    }
+    std::vector<void *> bufs;
+    int rc = 0;
+    auto copy = [&](uintptr_t from, uint64_t n) -> uint8_t * {
+        void *b = nullptr;
+        if (hipMallocAsync(&b, n ? n : 16, s) != hipSuccess) {
+            (void)hipGetLastError();
+            rc = -ENOMEM;
+            return nullptr;
+        }
+        bufs.push_back(b);
+        if (n && hipMemcpyAsync(b, (const void *)from, n, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+            (void)hipGetLastError();
+            rc = -EIO;
+        }
+        return static_cast<uint8_t *>(b);
+    };
+    if (same && hi - lo <= 2 * total) {
+        uint8_t *b = copy(lo, hi - lo);
+        for (u32 p = 0; rc == 0 && p < ECD_MAX_ROWS; ++p) {
+            const uintptr_t a = (uintptr_t)d->in_base[p];
+            if (a && (a & 15))
+                c->in_base[p] = b + (a - lo);
+        }
+    } else {
+        for (u32 p = 0; rc == 0 && p < ECD_MAX_ROWS; ++p) {
+            const uintptr_t a = (uintptr_t)d->in_base[p];
+            if (a && (a & 15))
+                c->in_base[p] = copy(a, span);
+        }
+    }
+    if (rc == 0)
+        rc = combine_any<NTS>(s, c.get());
+    for (void *b : bufs)
+        (void)hipFreeAsync(b, s);
+    return rc;
+}
+
+} // namespace
+
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
 {
     /* EC_MI355X_NTS=0: default-policy stores on the device path (A/B only) */
@@ -748,6 +869,8 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
         const char *e = getenv("EC_MI355X_NTS");
         return !(e && *e == '0');
     }();
+    if (inputs_misaligned(d))
+        return nts ? combine_realigned<true>(s, d) : combine_realigned<false>(s, d);
     return nts ? combine_any<true>(s, d) : combine_any<false>(s, d);
 }
 

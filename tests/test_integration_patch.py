@@ -1,8 +1,12 @@
 """The reference-side binding as a patch:
 integration/glusterfs-ec-mi355x.patch must apply cleanly (-p1) to the
-reference's xlators/cluster/ec/src/{Makefile.am, ec-method.h, ec.c}, drop
-every coding-layer source from ec.la, link libec_mi355x, and leave
-ec-method.h including the library header after ec-types.h.  Works on a
+reference's xlators/cluster/ec/src/{Makefile.am, ec-method.h, ec-types.h,
+ec.c} and libglusterfs/src/{iobuf.c, glusterfs/iobuf.h, libglusterfs.sym},
+drop every coding-layer source from ec.la, link libec_mi355x, leave
+ec-method.h including the library header after ec-types.h, keep every
+header ec.c includes in the distributed header list, and register the
+client's iobuf arenas with the coder (pinned, device-mapped: zero copy)
+after their mmap and unregister them before their munmap.  Works on a
 scratch copy; skipped where the reference tree is absent (the GPU box)."""
 import os
 import re
@@ -15,7 +19,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PATCH = os.path.join(ROOT, "integration", "glusterfs-ec-mi355x.patch")
 REF = "/root/reference"
 SUB = os.path.join("xlators", "cluster", "ec", "src")
-FILES = ("Makefile.am", "ec-method.h", "ec.c")
+LIBSRC = os.path.join("libglusterfs", "src")
+FILES = tuple(os.path.join(SUB, f) for f in ("Makefile.am", "ec-method.h", "ec-types.h",
+                                             "ec.c")) + \
+    tuple(os.path.join(LIBSRC, f) for f in ("iobuf.c", os.path.join("glusterfs", "iobuf.h"),
+                                           "libglusterfs.sym"))
 
 
 @pytest.fixture
@@ -25,9 +33,9 @@ def scratch(tmp_path):
     if shutil.which("patch") is None:
         pytest.skip("patch(1) not installed")
     d = tmp_path / "ref"
-    (d / SUB).mkdir(parents=True)
     for f in FILES:
-        shutil.copy(os.path.join(REF, SUB, f), d / SUB / f)
+        (d / f).parent.mkdir(parents=True, exist_ok=True)
+        shutil.copy(os.path.join(REF, f), d / f)
     return d
 
 
@@ -54,3 +62,42 @@ def test_patched_build_files(scratch):
     assert inc == ['#include "ec-types.h"', "#include <ec_method.h>"], inc
     assert not re.search(r"\bec_method_\w+\s*\(", hdr)   # prototypes come from the library
     assert '"avx", "hip"}' in (scratch / SUB / "ec.c").read_text()
+
+
+def test_patched_ec_includes_are_distributed(scratch):
+    """every local header the patched ec.c includes is either in
+    ec_headers (so `make dist` ships it) or provided by the library."""
+    subprocess.run(["patch", "-p1", "--batch", "-i", PATCH], cwd=scratch, check=True,
+                   capture_output=True)
+    mk = (scratch / SUB / "Makefile.am").read_text()
+    listed = set(re.findall(r"ec_headers [+:]= (\S+)", mk))
+    src = (scratch / SUB / "ec.c").read_text()
+    local = re.findall(r'^#include "([^"]+)"', src, re.M)
+    assert "ec-code.h" not in local and "ec-galois.h" not in local
+    for h in local:
+        assert h in listed, h
+    # nothing from the dropped coding headers is used by ec.c
+    for sym in ("ec_code_", "ec_gf_mul", "ec_gf_div", "EC_CODE_"):
+        assert sym not in src, sym
+
+
+def test_patched_iobuf_arena_hooks(scratch):
+    """the client's iobuf arenas are registered with the
+    coder after mmap and unregistered before munmap (iobuf.c:124, :157)."""
+    subprocess.run(["patch", "-p1", "--batch", "-i", PATCH], cwd=scratch, check=True,
+                   capture_output=True)
+    io = (scratch / LIBSRC / "iobuf.c").read_text()
+    m = io.index("mmap(NULL, iobuf_arena->arena_size")
+    assert io.index("iobuf_arena_reg(iobuf_arena->mem_base", m) > m
+    u = io.index("munmap(iobuf_arena->mem_base")
+    assert io.rindex("iobuf_arena_unreg(iobuf_arena->mem_base", 0, u) < u
+    assert "iobuf_set_arena_hooks(struct iobuf_pool *iobuf_pool" in io
+    hdr = (scratch / LIBSRC / "glusterfs" / "iobuf.h").read_text()
+    assert "typedef int (*iobuf_arena_hook_t)(void *base, size_t size);" in hdr
+    assert "iobuf_set_arena_hooks\n" in (scratch / LIBSRC / "libglusterfs.sym").read_text()
+    ec = (scratch / SUB / "ec.c").read_text()
+    assert "ec_method_host_register(base, size)" in ec
+    assert "ec_method_host_unregister(base)" in ec
+    assert "ec->iobuf_hooks = ec_iobuf_hooks_get(this, extensions);" in ec
+    assert "ec_iobuf_hooks_put(this);" in ec
+    assert "gf_boolean_t iobuf_hooks;" in (scratch / SUB / "ec-types.h").read_text()
