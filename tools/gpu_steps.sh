@@ -1,0 +1,34 @@
+#!/bin/bash
+# One gpurun call running a chosen list of steps at HEAD, each under its own
+# time limit, stopping at the first failure (no retries):
+#   TAG=r03a tools/gpu_steps.sh smoke pytest bench
+# Steps: smoke | pytest | pytest_new (the files in $TESTS) | bench | bench_rocprof
+#        | rehearsal (2 gloo ranks on GPU 0) | profile (per-config rocprof + PMC)
+#        | kbench (tools/kbench/kbench $KBENCH_ARGS)
+# Logs go to gpurun_out/${TAG}_<step>.log.
+set -u
+mkdir -p gpurun_out
+TAG=${TAG:-r03}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "[$(date +%T)] start $name"
+  timeout -k 10 "$to" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"; tail -4 "gpurun_out/${TAG}_$name.log" | cut -c1-600
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    pytest_new) run pytest_new 600 python -u -m pytest ${TESTS} -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    bench) run bench 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench_rocprof) run bench_rocprof 300 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_bench_$TAG -o run --output-format csv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-extra --no-cpu && python3 $R/tools/prof_filter.py $R/gpurun_out/prof_bench_$TAG ec_" ;;
+    rehearsal) run rehearsal 300 env EC_BENCH_BACKEND=gloo EC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1 ;;
+    profile) run profile 900 bash tools/profile.sh "$TAG" ${PROFILE_ARGS:-dec:4+2:3C 1 enc:4+2 1 enc:8+4 0.25 dec:8+4:FF0 0.25 enc:16+4 2 mixed:8+4 1 heal:8+4 1 dec:16+4:FFFF0 1 mixed:16+4:64 1 rmw:4+2 1} ;;
+    kbench) run kbench 600 tools/kbench/kbench ${KBENCH_ARGS:-} ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[$(date +%T)] done"
