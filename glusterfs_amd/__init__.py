@@ -8,7 +8,9 @@ from .ec_method import (  # noqa: F401
     EC_METHOD_MAX_FRAGMENTS,
     ECMatrixList,
     PinnedArray,
+    copy_threads,
     device_count,
+    device_numa_node,
     encode_matrix,
     gf_div,
     gf_mul,

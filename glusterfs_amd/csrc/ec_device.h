@@ -118,8 +118,14 @@ void ecd_inject_faults(uint32_t n);
  * memory `p`, or -1 for host memory (pageable or pinned). */
 int ecd_ptr_device(const void *p);
 
-/* Pinned host allocation helpers (zero-copy PCIe transfers). */
+/* Pinned host allocation helpers (zero-copy PCIe transfers); allocations
+ * are placed on the NUMA node of the first host-buffer device. */
 void *ecd_host_alloc(size_t bytes);
+/* NUMA node of device index `device` (-1: unknown / single node). */
+int ecd_device_numa_node(int device);
+/* Staging copy threads this process uses (EC_COPY_THREADS, else at most 8
+ * and at most the usable CPUs). */
+int ecd_copy_threads(void);
 void ecd_host_free(void *p);
 int ecd_host_register(void *p, size_t bytes);
 int ecd_host_unregister(void *p);

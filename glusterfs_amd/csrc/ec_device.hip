@@ -15,11 +15,16 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <ctype.h>
 #include <errno.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -27,6 +32,7 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -52,11 +58,28 @@ uint64_t pipe_batch_bytes()
     return v;
 }
 
+/* CPUs this process may use: its affinity, capped by the cgroup CPU quota
+ * (the GPU pool grants 16 CPUs of a 256-thread host; ranks of one job share
+ * it, so bench.py also sets EC_COPY_THREADS to its share per rank). */
+int usable_cpus()
+{
+    cpu_set_t cs;
+    int n = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : 1;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = "";
+        long per = 0;
+        if (fscanf(f, "%31s %ld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+            n = std::min<long>(n, std::max<long>(1, atol(q) / per));
+        fclose(f);
+    }
+    return std::max(n, 1);
+}
+
 int copy_threads()
 {
     static const int v = [] {
         const char *e = getenv("EC_COPY_THREADS");
-        const int t = e ? atoi(e) : 8;
+        const int t = e ? atoi(e) : std::min(8, usable_cpus());
         return std::min(std::max(t, 0), 64);
     }();
     return v;
@@ -352,6 +375,115 @@ uint8_t *mapped(const void *p, size_t n)
     return static_cast<uint8_t *>(d0);
 }
 
+/* ---------------------------------------------- NUMA-local pinned memory */
+
+/* NUMA node of device index `dev` (sysfs numa_node of its PCI function),
+ * -1 when unknown or on a single-node host. */
+int g_numa[kMaxDev];
+std::once_flag g_numa_once;
+
+int count_numa_nodes()
+{
+    int n = 0;
+    for (int i = 0; i < 1024; ++i) {
+        char path[64];
+        snprintf(path, sizeof path, "/sys/devices/system/node/node%d", i);
+        if (access(path, F_OK) != 0)
+            break;
+        ++n;
+    }
+    return n;
+}
+
+void discover_numa()
+{
+    const bool multi = count_numa_nodes() > 1;
+    for (int d = 0; d < kMaxDev; ++d)
+        g_numa[d] = -1;
+    for (int d = 0; d < g_ndev; ++d) {
+        char bus[64] = "", path[128];
+        if (hipDeviceGetPCIBusId(bus, sizeof bus, g_dev_ids[d]) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        for (char *c = bus; *c; ++c)
+            *c = (char)tolower((unsigned char)*c);
+        snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+        if (FILE *f = fopen(path, "r")) {
+            int node = -1;
+            if (fscanf(f, "%d", &node) == 1 && node >= 0)
+                g_numa[d] = multi || getenv("EC_NUMA_FORCE") ? node : -1;
+            fclose(f);
+        }
+    }
+}
+
+int device_numa(int dev)
+{
+    std::call_once(g_numa_once, discover_numa);
+    return dev >= 0 && dev < g_ndev ? g_numa[dev] : -1;
+}
+
+/* Pinned, device-mapped host memory whose pages sit on NUMA node `node`:
+ * an anonymous mapping bound (preferred) to the node, faulted in there,
+ * then registered with the HIP runtime.  hipHostMalloc places pages by the
+ * calling thread's first touch, i.e. wherever the caller happens to run --
+ * on a 2-socket host half the ranks would stage across the socket link.
+ * Node < 0, or any step failing: hipHostMalloc. */
+std::mutex g_numa_mu;
+std::map<void *, size_t> g_numa_allocs;
+
+void *pinned_alloc(size_t bytes, int node)
+{
+    bytes = bytes ? bytes : 1;
+    if (node >= 0 && node < 1024 && !getenv("EC_NUMA_OFF")) {
+        const size_t pg = 4096, len = (bytes + pg - 1) / pg * pg;
+        void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p != MAP_FAILED) {
+            unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {};
+            mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+            /* MPOL_PREFERRED (1): the node if it has room, else anywhere */
+            (void)syscall(SYS_mbind, p, len, 1, mask, (unsigned long)1024, 0u);
+            memset(p, 0, len);                       /* fault in on the node */
+            if (hipHostRegister(p, len, hipHostRegisterMapped) == hipSuccess) {
+                std::lock_guard<std::mutex> g(g_numa_mu);
+                g_numa_allocs[p] = len;
+                return p;
+            }
+            (void)hipGetLastError();
+            munmap(p, len);
+        }
+    }
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void pinned_free(void *p)
+{
+    if (!p)
+        return;
+    size_t len = 0;
+    {
+        std::lock_guard<std::mutex> g(g_numa_mu);
+        auto it = g_numa_allocs.find(p);
+        if (it != g_numa_allocs.end()) {
+            len = it->second;
+            g_numa_allocs.erase(it);
+        }
+    }
+    if (len) {
+        (void)hipHostUnregister(p);
+        munmap(p, len);
+    } else {
+        (void)hipHostFree(p);
+    }
+    g_host_gen.fetch_add(1, std::memory_order_release);
+}
+
 /* Per-device pipeline resources (pooled). */
 constexpr int kSlots = 2;
 
@@ -369,19 +501,24 @@ struct Stage {
 std::mutex g_pool_mu;
 std::vector<Stage *> g_pool[kMaxDev];
 
-int grow(uint8_t *(&slot)[kSlots], size_t &cap, size_t want)
+int grow(uint8_t *(&slot)[kSlots], size_t &cap, size_t want, int dev)
 {
     if (want <= cap)
         return 0;
     for (auto &p : slot)
         if (p) {
-            (void)hipHostFree(p);
+            pinned_free(p);
             p = nullptr;
-            g_host_gen.fetch_add(1, std::memory_order_release);
         }
     cap = 0;
-    for (auto &p : slot)
-        HIPCHK(hipHostMalloc(&p, want, hipHostMallocDefault));
+    for (auto &p : slot) {
+        p = static_cast<uint8_t *>(pinned_alloc(want, device_numa(dev)));
+        if (!p) {
+            std::lock_guard<std::mutex> g(g_err_mu);
+            g_err = "pinned staging allocation failed";
+            return -ENOMEM;
+        }
+    }
     cap = want;
     return 0;
 }
@@ -553,9 +690,9 @@ int run_encode_dev(int dev, const EncodeJob &j)
     Stage *s = acquire(dev);
     if (!s)
         return -EIO;
-    int rc = grow(s->pin_in, s->cap_in, in_direct ? 0 : B * stripe_in);
+    int rc = grow(s->pin_in, s->cap_in, in_direct ? 0 : B * stripe_in, dev);
     if (rc == 0)
-        rc = grow(s->pin_out, s->cap_out, all_direct ? 0 : B * j.n * ECD_CHUNK);
+        rc = grow(s->pin_out, s->cap_out, all_direct ? 0 : B * j.n * ECD_CHUNK, dev);
     const uint64_t nb = (cnt_all + B - 1) / B;
     if (rc == 0)
         rc = run_pipeline(s, nb, [&](uint64_t b, int slot, Batch &bt) {
@@ -628,11 +765,11 @@ int run_decode_dev(int dev, const DecodeJob &j)
     Stage *s = acquire(dev);
     if (!s)
         return -EIO;
-    int rc = grow(s->pin_in, s->cap_in, any_in_staged ? Bs * j.nfrags * ECD_CHUNK : 0);
+    int rc = grow(s->pin_in, s->cap_in, any_in_staged ? Bs * j.nfrags * ECD_CHUNK : 0, dev);
     if (rc == 0)
-        rc = grow(s->pin_out, s->cap_out, all_direct ? 0 : Bs * out_stripe);
+        rc = grow(s->pin_out, s->cap_out, all_direct ? 0 : Bs * out_stripe, dev);
     if (rc == 0)
-        rc = grow(s->pin_grp, s->cap_grp, j.group_pattern ? (Bs + grp - 1) / grp + 1 : 0);
+        rc = grow(s->pin_grp, s->cap_grp, j.group_pattern ? (Bs + grp - 1) / grp + 1 : 0, dev);
     const uint64_t nb = (cnt_all + B - 1) / B;
     if (rc == 0)
         rc = run_pipeline(s, nb, [&](uint64_t b, int slot, Batch &bt) {
@@ -1070,22 +1207,30 @@ int ecd_ptr_device(const void *p)
     return -1;
 }
 
+/* On the NUMA node of the first host-buffer device (EC_MI355X_HOST_DEVICES:
+ * one rank per GPU gets its own GPU's node). */
 void *ecd_host_alloc(size_t bytes)
 {
     if (ecd_device_count() == 0)
         return nullptr;
-    void *p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
-        return nullptr;
-    return p;
+    return pinned_alloc(bytes, device_numa(g_host_devs[0]));
 }
 
 void ecd_host_free(void *p)
 {
-    if (p) {
-        (void)hipHostFree(p);
-        g_host_gen.fetch_add(1, std::memory_order_release);
-    }
+    pinned_free(p);
+}
+
+int ecd_device_numa_node(int device)
+{
+    if (ecd_device_count() <= device || device < 0)
+        return -ENODEV;
+    return device_numa(device);
+}
+
+int ecd_copy_threads(void)
+{
+    return copy_threads();
 }
 
 int ecd_host_register(void *p, size_t bytes)

@@ -329,6 +329,168 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile(const uint8_t *__restr
     }
 }
 
+/* Narrow-tile encoder (r03): T = 4 or 8 stripes per block, one wave item
+ * per fragment row (CW = T / 4 dwords per plane per lane, so an item covers
+ * the tile's T stripes), NW waves per block.  At k = 16 the 8-stripe tile is
+ * 64 KiB of LDS and only two blocks fit a CU, whose load / compute / store
+ * phases then line up; T = 4 halves the tile so up to five blocks share a
+ * CU.  WOT: each wave assembles its row's T chunks in a private LDS slice
+ * and stores them as one contiguous T * 512-byte run (16 B per lane), not as
+ * 64-B plane segments at a 512-B stride (PMC: 1.06-1.10x write bytes for
+ * the segment stores of the 8+4 encoder). */
+template <int K, int I, bool DIRECT, int CW, int T>
+__device__ __forceinline__ void encode_tile_acc(const uint8_t *col, u32 (&acc)[8][CW])
+{
+    constexpr u32 v = I + 1;
+    u32 y[8][CW];
+    if constexpr (DIRECT && v != 1) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int w = 0; w < CW; ++w)
+                acc[b][w] = 0;
+        static_for<0, K>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const uint8_t *src = col + (u32)j * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+            ecgf::mul_xor<gf_pow_c(v, K - 1 - j), CW, true>(acc, acc, y);
+        });
+    } else {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            load_plane<CW>(col + (u32)b * (T * 64u), acc[b]);
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+            const uint8_t *src = col + (u32)j * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+            if constexpr (v == 1) {
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+#pragma unroll
+                    for (int w = 0; w < CW; ++w)
+                        acc[b][w] ^= y[b][w];
+            } else {
+                ecgf::horner<v, CW, true>(acc, y);
+            }
+        }
+    }
+}
+
+/* Stage the tile's k input chunks (stripes t0 .. t0+T-1, any that exist) into
+ * the plane-major LDS tile by LDS-DMA: input p, plane b, stripe s at
+ * ((p * 8 + b) * T + s) * 64; a wave instruction fills 1 KiB. */
+template <int T, int NW>
+__device__ __forceinline__ void stage_tile(uint8_t *lds, const uint8_t *const *base,
+                                           uint64_t stride, u32 k, uint64_t t0,
+                                           uint64_t nstripes, u32 wave, u32 lane)
+{
+    constexpr u32 PER = T / 2;                 /* wave instructions per input */
+    const u32 ni = k * PER;
+    for (u32 ins = wave; ins < ni; ins += NW) {
+        const u32 p = ins / PER;
+        const u32 el = (ins % PER) * 64 + lane;  /* 16-B piece within input p */
+        const u32 seg = el >> 2;
+        const uint64_t st = t0 + seg % T;
+        if (st < nstripes) {
+            const uint8_t *g = base[p] + st * stride + (seg / T) * 64u + (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+        }
+    }
+}
+
+/* wave-local LDS hand-off (the slice is private to the wave) */
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* Write the wave's T chunks (lane (cs, cc) holds column cc of stripe cs, CW
+ * dwords per plane) through its LDS slice as contiguous 16-B lane pieces:
+ * chunk s goes to dst(s) + [0, 512).  dst(s) = nullptr: no stripe. */
+template <int T, int CW, bool NTS, typename D>
+__device__ __forceinline__ void store_chunks_via_lds(uint8_t *slice, const u32 (&acc)[8][CW],
+                                                     u32 cs, u32 cc, u32 lane, D dst)
+{
+    uint8_t *o = slice + cs * ECD_CHUNK + cc * (4u * CW);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        if constexpr (CW == 1)
+            *reinterpret_cast<u32 *>(o + b * 64) = acc[b][0];
+        else
+            *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (u32 j = 0; j < T * ECD_CHUNK / 1024; ++j) {
+        const u32 off = (j * 64 + lane) * 16;
+        uint8_t *d = dst(off / ECD_CHUNK);
+        if (d) {
+            const v4u v = *reinterpret_cast<const v4u *>(slice + off);
+            if constexpr (NTS)
+                __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(d + off % ECD_CHUNK));
+            else
+                *reinterpret_cast<v4u *>(d + off % ECD_CHUNK) = v;
+        }
+    }
+    wave_lds_sync();
+}
+
+template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT>
+__global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const uint8_t *__restrict__ in,
+                                                            const FragPtrs out,
+                                                            uint64_t nstripes)
+{
+    static_assert(T == 4 || T == 8, "4- or 8-stripe tiles");
+    constexpr int CW = T / 4;
+    constexpr u32 LPS = 16 / CW;               /* lanes per stripe */
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const uint8_t *base[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p)
+        base[p] = in + (uint64_t)p * ECD_CHUNK;
+    stage_tile<T, NW>(lds, base, (uint64_t)K * ECD_CHUNK, K, t0, nstripes, wave, lane);
+    __syncthreads();
+    const u32 cs = lane / LPS, cc = lane % LPS;
+    const uint8_t *col = lds + cs * 64u + cc * (4u * CW);
+    uint8_t *slice = lds + K * T * ECD_CHUNK + wave * T * ECD_CHUNK;
+    const uint64_t ost = t0 + cs;
+    for (u32 r = wave; r < (u32)N; r += NW) {
+        const u32 ru = __builtin_amdgcn_readfirstlane(r);
+        static_for<0, N>([&](auto I) {
+            if (ru == (u32)decltype(I)::value) {
+                u32 acc[8][CW];
+                encode_tile_acc<K, decltype(I)::value, DIRECT, CW, T>(col, acc);
+                uint8_t *row = out.p[decltype(I)::value];
+                if constexpr (WOT) {
+                    store_chunks_via_lds<T, CW, NTS>(slice, acc, cs, cc, lane, [&](u32 s) {
+                        return t0 + s < nstripes ? row + (t0 + s) * ECD_CHUNK : nullptr;
+                    });
+                } else if (ost < nstripes) {
+                    store_chunk<CW, NTS>(row + ost * ECD_CHUNK + cc * (4u * CW), acc);
+                }
+            }
+        });
+    }
+}
+
+template <int T, int NW, bool WOT>
+constexpr size_t encode_tile_t_lds(int k)
+{
+    return (size_t)k * T * ECD_CHUNK + (WOT ? (size_t)NW * T * ECD_CHUNK : 0);
+}
+
 template <int W>
 inline uint64_t vander_grid(uint64_t nstripes)
 {
@@ -796,6 +958,75 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                 *reinterpret_cast<v4u *>(dst) = v;
         }
     }
+}
+
+/* Narrow-tile combine (r03): ec_combine's decode / heal / mixed kernel with
+ * T = 4 stripes per block and one dword per plane per lane (16 lanes per
+ * stripe), so a k = 16 tile is 32 KiB and four 8-wave blocks share a CU.
+ * Each wave item is one output row for the 4 stripes; the multiply jumps
+ * into the one-dword bodies of ec_gf8_asm.h.  WOT as in ec_encode_tile_t:
+ * the row's 4 chunks leave through the wave's LDS slice in 512-B runs. */
+template <int K, int NW, bool MIXED, bool NTS, bool WOT>
+__global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
+{
+    constexpr u32 T = 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
+    const uint8_t *base[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p)
+        base[p] = (u32)p < k ? a.in_base[pw.byte(a, p)] : nullptr;
+    stage_tile<T, NW>(lds, base, a.in_stride, k, t0, a.nstripes, wave, lane);
+    __syncthreads();
+    const u32 cs = lane >> 4, cc = lane & 15u;
+    const uint8_t *col = lds + cs * 64u + cc * 4u;
+    uint8_t *slice = lds + K * T * ECD_CHUNK + wave * T * ECD_CHUNK;
+    const uint64_t ost = t0 + cs;
+    for (u32 r = wave; r < a.rows; r += NW) {
+        const u32 rw = a.kw * (1 + r);
+        const u32 w0 = pw.word(a, rw);
+        const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+        const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
+        const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
+        u32 acc[8][1], y[8][1];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc[b][0] = 0;
+        uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
+#pragma unroll 1
+        for (u32 p = 0; p < k; ++p) {
+            const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+            cl = (cl >> 8) | (ch << 56);
+            ch >>= 8;
+            if (c == 0)                  /* ec-code-c.c:11666-11676 */
+                continue;
+            const uint8_t *src = col + p * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                y[b][0] = *reinterpret_cast<const u32 *>(src + (u32)b * (T * 64u));
+            u32 t[ECGF_ASM_TEMPS][1];
+            ECGF_ASM_DISPATCH_W1(acc, y, t, c);
+        }
+        if constexpr (WOT) {
+            store_chunks_via_lds<T, 1, NTS>(slice, acc, cs, cc, lane, [&](u32 s) {
+                return t0 + s < a.nstripes ? a.out_base[r] + (t0 + s) * a.out_stride : nullptr;
+            });
+        } else if (ost < a.nstripes) {
+            store_chunk<1, NTS>(a.out_base[r] + ost * a.out_stride + cc * 4u, acc);
+        }
+    }
+}
+
+template <int NW, bool WOT>
+constexpr size_t combine_n_lds(int k)
+{
+    return (size_t)k * 4 * ECD_CHUNK + (WOT ? (size_t)NW * 4 * ECD_CHUNK : 0);
 }
 
 /* Zero-copy variant for the host-buffer path, where every input and output

@@ -677,6 +677,18 @@ ec_method_device_count(void)
     return ecd_device_count();
 }
 
+int32_t
+ec_method_device_numa_node(int32_t device)
+{
+    return ecd_device_numa_node(device);
+}
+
+int32_t
+ec_method_copy_threads(void)
+{
+    return ecd_copy_threads();
+}
+
 const char *
 ec_method_last_error(void)
 {

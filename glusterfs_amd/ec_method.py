@@ -39,7 +39,7 @@ EXPORTS = (
     "ec_method_gf_div", "ec_method_config_fill", "ec_method_config_pack",
     "ec_method_config_unpack", "ec_method_config_check", "ec_method_writev_encode",
     "ec_method_writev_encode_device", "ec_method_engine", "ec_method_get_stats",
-    "ec_method_inject_device_faults",
+    "ec_method_inject_device_faults", "ec_method_device_numa_node", "ec_method_copy_threads",
 )
 
 
@@ -134,6 +134,8 @@ def _load():
         "ec_method_heal_device": (i32, [P, ctypes.c_int, vp, u64, up, vp, up, vp]),
         "ec_method_sync_device": (i32, [ctypes.c_int, vp]),
         "ec_method_device_count": (i32, []),
+        "ec_method_device_numa_node": (i32, [i32]),
+        "ec_method_copy_threads": (i32, []),
         "ec_method_last_error": (ctypes.c_char_p, []),
         "ec_method_host_alloc": (vp, [ctypes.c_size_t]),
         "ec_method_host_free": (None, [vp]),
@@ -191,6 +193,16 @@ def _check(rc, what):
 
 def device_count():
     return lib.ec_method_device_count()
+
+
+def device_numa_node(device):
+    """NUMA node of gfx950 device `device` (-1: unknown / one-node host)."""
+    return lib.ec_method_device_numa_node(device)
+
+
+def copy_threads():
+    """Staging copy threads of this process (ec_method_copy_threads)."""
+    return lib.ec_method_copy_threads()
 
 
 def stats():

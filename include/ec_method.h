@@ -243,6 +243,13 @@ int32_t ec_method_config_check(uint32_t bricks, uint32_t redundancy,
 
 /* Number of visible gfx950 devices (0 = CPU engine only). */
 int32_t ec_method_device_count(void);
+/* NUMA node of gfx950 device `device` (-1: unknown or a one-node host,
+ * -ENODEV: no such device): where a client should run the threads that
+ * fill its buffers, and where ec_method_host_alloc places its pages. */
+int32_t ec_method_device_numa_node(int32_t device);
+/* CPU threads the library uses to stage pageable buffers: EC_COPY_THREADS,
+ * else min(8, CPUs usable by the process -- affinity and cgroup quota). */
+int32_t ec_method_copy_threads(void);
 /* The engine a volume's coder runs ("gfx950 x8 + cpu/avx512", "cpu/avx2"...),
  * as logged by ec_method_init (cf. ec-code.c:1048-1053). */
 const char *ec_method_engine(const ec_matrix_list_t *list);
@@ -264,7 +271,9 @@ void ec_method_inject_device_faults(uint32_t count);
 const char *ec_method_last_error(void);
 /* Pinned, device-mapped host memory.  Host buffers in such memory (16-byte
  * aligned) are coded in place by the GPU over PCIe with no staging copy;
- * pageable buffers are staged through pinned slots by CPU threads. */
+ * pageable buffers are staged through pinned slots by CPU threads.  The
+ * pages are placed on the NUMA node of the first host-buffer GPU
+ * (EC_MI355X_HOST_DEVICES), as are the staging slots of each GPU. */
 void *ec_method_host_alloc(size_t bytes);
 void ec_method_host_free(void *p);
 /* Pin and map an existing host range (e.g. a GlusterFS iobuf arena, see

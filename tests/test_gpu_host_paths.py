@@ -224,7 +224,9 @@ def _attr_queries(kind):
         "    arrs = [np.zeros(512 * 4 * 8, np.uint8)] + [np.zeros(512 * 8, np.uint8) for _ in range(6)]\n"
         "for _ in range(4):\n"
         "    L.encode_batch(8, arrs[0], arrs[1:])\n" % kind)
-    env = dict(os.environ, EC_MI355X_DEBUG="1", EC_MI355X_QUIET="1")
+    # (a lifetime longer than the run: the entries' expiry is
+    # test_gpu_guards.py's subject)
+    env = dict(os.environ, EC_MI355X_DEBUG="1", EC_MI355X_QUIET="1", EC_HOSTPAGE_MS="10000")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]

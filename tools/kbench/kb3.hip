@@ -1,0 +1,292 @@
+/*
+ * kb3.hip -- round-3 development harness (not product): A/B of the
+ * narrow-tile kernels (ec_encode_tile_t, ec_combine_n) against the shipped
+ * instantiations, in ONE process with interleaved rounds and the median of
+ * rounds; every variant's output is compared with its group's first.
+ *
+ *   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I glusterfs_amd/csrc \
+ *         tools/kbench/kb3.hip -o tools/kbench/kb3
+ *   tools/kbench/kb3 [GiB=1] [rounds=7] [groups=all|enc16,enc8,...]
+ */
+#include "../../glusterfs_amd/csrc/ec_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CHK(x)                                                                             \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);  \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+struct Variant {
+    std::string name;
+    double bytes;
+    std::function<void(hipStream_t)> fn;
+    uint8_t *out;
+    size_t out_bytes;
+};
+
+static void fill(uint8_t *d, size_t n, uint32_t seed)
+{
+    std::vector<uint32_t> h(n / 4);
+    uint32_t x = seed | 1;
+    for (auto &w : h) {
+        x ^= x << 13;
+        x ^= x >> 17;
+        x ^= x << 5;
+        w = x;
+    }
+    CHK(hipMemcpy(d, h.data(), n, hipMemcpyHostToDevice));
+}
+
+static void run_group(const char *title, std::vector<Variant> &vars, int rounds, int iters,
+                      hipStream_t s)
+{
+    std::vector<uint8_t> ref, cur;
+    for (size_t v = 0; v < vars.size(); ++v) {
+        if (!vars[v].out)
+            continue;
+        CHK(hipMemset(vars[v].out, 0, vars[v].out_bytes));
+        vars[v].fn(s);
+        CHK(hipStreamSynchronize(s));
+        cur.resize(vars[v].out_bytes);
+        CHK(hipMemcpy(cur.data(), vars[v].out, vars[v].out_bytes, hipMemcpyDeviceToHost));
+        if (ref.empty())
+            ref = cur;
+        else if (cur != ref)
+            printf("  MISMATCH %s\n", vars[v].name.c_str());
+    }
+    hipEvent_t e0, e1;
+    CHK(hipEventCreate(&e0));
+    CHK(hipEventCreate(&e1));
+    std::vector<std::vector<double>> t(vars.size());
+    for (int rd = 0; rd < rounds; ++rd)
+        for (size_t v = 0; v < vars.size(); ++v) {
+            for (int i = 0; i < 3; ++i)
+                vars[v].fn(s);
+            CHK(hipEventRecord(e0, s));
+            for (int i = 0; i < iters; ++i)
+                vars[v].fn(s);
+            CHK(hipEventRecord(e1, s));
+            CHK(hipEventSynchronize(e1));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            t[v].push_back(ms / iters);
+        }
+    printf("== %s\n%-40s %9s %9s %9s %7s\n", title, "variant", "ms(med)", "ms(min)", "GB/s",
+           "frac8T");
+    for (size_t v = 0; v < vars.size(); ++v) {
+        std::sort(t[v].begin(), t[v].end());
+        const double med = t[v][t[v].size() / 2];
+        printf("%-40s %9.4f %9.4f %9.1f %7.3f\n", vars[v].name.c_str(), med, t[v][0],
+               vars[v].bytes / med / 1e6, vars[v].bytes / med / 1e6 / 8000.0);
+    }
+    fflush(stdout);
+    CHK(hipEventDestroy(e0));
+    CHK(hipEventDestroy(e1));
+}
+
+static bool want(const char *groups, const char *g)
+{
+    if (!groups || !strcmp(groups, "all"))
+        return true;
+    std::string s = std::string(",") + groups + ",";
+    return s.find(std::string(",") + g + ",") != std::string::npos;
+}
+
+static void lds_attr(const void *kern, size_t bytes)
+{
+    if (bytes > (64u << 10))
+        CHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
+
+static FragPtrs frag_ptrs(uint8_t *b, uint64_t nst, int n)
+{
+    FragPtrs f;
+    for (int i = 0; i < n; ++i)
+        f.p[i] = b + (uint64_t)i * nst * ECD_CHUNK;
+    return f;
+}
+
+/* shipped device encode path (ecdk_encode_vander) */
+static void add_shipped_encode(std::vector<Variant> &v, const char *nm, int k, int n,
+                               uint64_t nst, const uint8_t *in, FragPtrs f)
+{
+    v.push_back({nm, (double)nst * (k + n) * ECD_CHUNK, [=](hipStream_t st) {
+                     void *o[ECD_MAX_ROWS];
+                     for (int i = 0; i < n; ++i)
+                         o[i] = f.p[i];
+                     if (ecdk_encode_vander(st, k, n, nst, in, o, false))
+                         exit(7);
+                 }, f.p[n - 1], (size_t)nst * ECD_CHUNK});
+}
+
+template <int K, int N, int T, int NW, bool DIRECT, bool WOT>
+static void add_tile_t(std::vector<Variant> &v, const char *nm, uint64_t nst, const uint8_t *in,
+                       FragPtrs f)
+{
+    auto kern = ec_encode_tile_t<K, N, T, NW, true, DIRECT, WOT>;
+    const size_t lds = encode_tile_t_lds<T, NW, WOT>(K);
+    lds_attr((const void *)kern, lds);
+    const uint64_t g = (nst + T - 1) / T;
+    v.push_back({nm, (double)nst * (K + N) * ECD_CHUNK, [=](hipStream_t st) {
+                     hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, in, f, nst);
+                 }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+}
+
+/* decode desc: k inputs (fragments), `rows` outputs, dense coefficients */
+static CombineArgs *make_args(int k, int rows, uint64_t nst, uint8_t *const *frags, uint8_t *out,
+                              bool stripe_major, const uint8_t *coef)
+{
+    ecd_combine_desc_t d;
+    memset(&d, 0, sizeof(d));
+    d.k = k;
+    d.rows = rows;
+    d.nstripes = nst;
+    d.in_stride = ECD_CHUNK;
+    d.out_stride = stripe_major ? (uint64_t)rows * ECD_CHUNK : ECD_CHUNK;
+    for (int p = 0; p < k; ++p) {
+        d.in_base[p] = frags[p];
+        d.pat[p] = (uint8_t)p;
+    }
+    for (int r = 0; r < rows; ++r)
+        d.out_base[r] = stripe_major ? out + (uint64_t)r * ECD_CHUNK : out + (uint64_t)r * nst * ECD_CHUNK;
+    memcpy(d.pat + k, coef, (size_t)rows * k);
+    d.npatterns = 1;
+    d.pat_bytes = k + rows * k;
+    CombineArgs *a = new CombineArgs;
+    if (ecdk_pack_args(&d, a))
+        exit(2);
+    return a;
+}
+
+static void add_shipped_combine(std::vector<Variant> &v, const char *nm, const CombineArgs *a,
+                                double bytes, uint8_t *out, size_t ob)
+{
+    v.push_back({nm, bytes, [=](hipStream_t st) {
+                     if (launch_combine_k<true>(st, *a))
+                         exit(8);
+                 }, out, ob});
+}
+
+template <int K, int NW, bool WOT>
+static void add_combine_n(std::vector<Variant> &v, const char *nm, const CombineArgs *a,
+                          double bytes, uint8_t *out, size_t ob)
+{
+    auto kern = ec_combine_n<K, NW, false, true, WOT>;
+    const size_t lds = combine_n_lds<NW, WOT>(K);
+    lds_attr((const void *)kern, lds);
+    const uint64_t g = (a->nstripes + 3) / 4;
+    v.push_back({nm, bytes, [=](hipStream_t st) {
+                     hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, *a);
+                 }, out, ob});
+}
+
+int main(int argc, char **argv)
+{
+    const double gib = argc > 1 ? atof(argv[1]) : 1.0;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 7;
+    const char *groups = argc > 3 ? argv[3] : "all";
+    const int iters = 10;
+    hipDeviceProp_t prop;
+    CHK(hipGetDeviceProperties(&prop, 0));
+    printf("device %s CUs %d, %.2f GiB user data per launch\n", prop.gcnArchName,
+           prop.multiProcessorCount, gib);
+    hipStream_t s;
+    CHK(hipStreamCreate(&s));
+    const uint64_t user = (uint64_t)(gib * (1ull << 30));
+    uint8_t *bufA, *bufB;
+    CHK(hipMalloc(&bufA, user * 2));
+    CHK(hipMalloc(&bufB, user * 2));
+    fill(bufA, user * 2, 12345);
+    std::vector<Variant> v;
+
+    if (want(groups, "enc16")) {
+        const uint64_t nst = user / (16 * ECD_CHUNK);
+        FragPtrs f = frag_ptrs(bufB, nst, 20);
+        add_shipped_encode(v, "shipped (tile T8 CW1 NW16)", 16, 20, nst, bufA, f);
+        add_tile_t<16, 20, 8, 10, false, false>(v, "T8 NW10", nst, bufA, f);
+        add_tile_t<16, 20, 8, 10, false, true>(v, "T8 NW10 WOT", nst, bufA, f);
+        add_tile_t<16, 20, 4, 4, false, false>(v, "T4 NW4", nst, bufA, f);
+        add_tile_t<16, 20, 4, 4, false, true>(v, "T4 NW4 WOT", nst, bufA, f);
+        add_tile_t<16, 20, 4, 5, false, false>(v, "T4 NW5", nst, bufA, f);
+        add_tile_t<16, 20, 4, 5, false, true>(v, "T4 NW5 WOT", nst, bufA, f);
+        add_tile_t<16, 20, 4, 10, false, false>(v, "T4 NW10", nst, bufA, f);
+        add_tile_t<16, 20, 4, 10, false, true>(v, "T4 NW10 WOT", nst, bufA, f);
+        add_tile_t<16, 20, 4, 5, true, false>(v, "T4 NW5 direct", nst, bufA, f);
+        run_group("encode 16+4", v, rounds, iters, s);
+        v.clear();
+    }
+    if (want(groups, "enc8")) {
+        for (int big = 0; big < 2; ++big) {
+            const uint64_t nst = big ? user / (8 * ECD_CHUNK) : 65536;
+            FragPtrs f = frag_ptrs(bufB, nst, 12);
+            add_shipped_encode(v, big ? "shipped (tile T8 CW2 NW16 direct)" : "shipped (vander W1)",
+                               8, 12, nst, bufA, f);
+            add_tile_t<8, 12, 8, 6, true, false>(v, "T8 NW6 direct", nst, bufA, f);
+            add_tile_t<8, 12, 8, 6, true, true>(v, "T8 NW6 direct WOT", nst, bufA, f);
+            add_tile_t<8, 12, 8, 12, true, true>(v, "T8 NW12 direct WOT", nst, bufA, f);
+            add_tile_t<8, 12, 4, 4, true, false>(v, "T4 NW4 direct", nst, bufA, f);
+            add_tile_t<8, 12, 4, 4, true, true>(v, "T4 NW4 direct WOT", nst, bufA, f);
+            add_tile_t<8, 12, 4, 6, true, true>(v, "T4 NW6 direct WOT", nst, bufA, f);
+            add_tile_t<8, 12, 4, 6, false, true>(v, "T4 NW6 WOT", nst, bufA, f);
+            add_tile_t<8, 12, 4, 12, true, true>(v, "T4 NW12 direct WOT", nst, bufA, f);
+            run_group(big ? "encode 8+4 (size = GiB arg)" : "encode 8+4, 64K stripes", v, rounds,
+                      iters, s);
+            v.clear();
+        }
+    }
+    if (want(groups, "enc4")) {
+        const uint64_t nst = user / (4 * ECD_CHUNK);
+        FragPtrs f = frag_ptrs(bufB, nst, 6);
+        add_shipped_encode(v, "shipped (combine NW16 jt)", 4, 6, nst, bufA, f);
+        add_tile_t<4, 6, 8, 6, true, true>(v, "T8 NW6 direct WOT", nst, bufA, f);
+        add_tile_t<4, 6, 8, 6, false, true>(v, "T8 NW6 WOT", nst, bufA, f);
+        add_tile_t<4, 6, 4, 6, true, true>(v, "T4 NW6 direct WOT", nst, bufA, f);
+        add_tile_t<4, 6, 4, 3, true, true>(v, "T4 NW3 direct WOT", nst, bufA, f);
+        add_tile_t<4, 6, 8, 6, true, false>(v, "T8 NW6 direct", nst, bufA, f);
+        run_group("encode 4+2", v, rounds, iters, s);
+        v.clear();
+    }
+    auto decode_group = [&](auto kk, const char *title, bool heal) {
+        constexpr int K = decltype(kk)::value;
+        const int rows = heal ? 4 : K;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        uint8_t *fr[16];
+        for (int p = 0; p < K; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)(1 + (i * 173 + 11) % 255);
+        const CombineArgs *a = make_args(K, rows, nst, fr, bufB, !heal, c);
+        const double bytes = (double)nst * (K + rows) * ECD_CHUNK;
+        const size_t ob = (size_t)nst * rows * ECD_CHUNK;
+        add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
+        add_combine_n<K, 8, false>(v, "narrow NW8", a, bytes, bufB, ob);
+        add_combine_n<K, 8, true>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
+        add_combine_n<K, 4, false>(v, "narrow NW4", a, bytes, bufB, ob);
+        add_combine_n<K, 4, true>(v, "narrow NW4 WOT", a, bytes, bufB, ob);
+        add_combine_n<K, 16, false>(v, "narrow NW16", a, bytes, bufB, ob);
+        run_group(title, v, rounds, iters, s);
+        v.clear();
+    };
+    if (want(groups, "dec16"))
+        decode_group(std::integral_constant<int, 16>{}, "decode 16+4 dense", false);
+    if (want(groups, "dec8"))
+        decode_group(std::integral_constant<int, 8>{}, "decode 8+4 dense", false);
+    if (want(groups, "heal8"))
+        decode_group(std::integral_constant<int, 8>{}, "heal 8+4 (4 rows)", true);
+    if (want(groups, "dec4"))
+        decode_group(std::integral_constant<int, 4>{}, "decode 4+2 dense", false);
+    CHK(hipFree(bufA));
+    CHK(hipFree(bufB));
+    return 0;
+}
