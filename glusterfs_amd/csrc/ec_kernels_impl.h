@@ -358,15 +358,31 @@ __device__ __forceinline__ void encode_tile_acc(const uint8_t *col, u32 (&acc)[8
             ecgf::mul_xor<gf_pow_c(v, K - 1 - j), CW, true>(acc, acc, y);
         });
     } else {
+        /* software-pipelined by hand: input j+1's planes are read while the
+         * Horner step of input j runs, and no further (scheduling barriers):
+         * left alone the scheduler issued all k x 8 reads of a row first,
+         * 88-136 VGPRs, 3-5 waves per SIMD */
+        u32 nx[8][CW];
 #pragma unroll
         for (int b = 0; b < 8; ++b)
             load_plane<CW>(col + (u32)b * (T * 64u), acc[b]);
 #pragma unroll
+        for (int b = 0; b < 8; ++b)
+            load_plane<CW>(col + (u32)(T * ECD_CHUNK) + (u32)b * (T * 64u), nx[b]);
+#pragma unroll
         for (int j = 1; j < K; ++j) {
-            const uint8_t *src = col + (u32)j * (T * ECD_CHUNK);
 #pragma unroll
             for (int b = 0; b < 8; ++b)
-                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+#pragma unroll
+                for (int w = 0; w < CW; ++w)
+                    y[b][w] = nx[b][w];
+            if (j + 1 < K) {
+                const uint8_t *src = col + (u32)(j + 1) * (T * ECD_CHUNK);
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    load_plane<CW>(src + (u32)b * (T * 64u), nx[b]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
             if constexpr (v == 1) {
 #pragma unroll
                 for (int b = 0; b < 8; ++b)
@@ -376,6 +392,7 @@ __device__ __forceinline__ void encode_tile_acc(const uint8_t *col, u32 (&acc)[8
             } else {
                 ecgf::horner<v, CW, true>(acc, y);
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
@@ -383,11 +400,13 @@ __device__ __forceinline__ void encode_tile_acc(const uint8_t *col, u32 (&acc)[8
 /* Stage the tile's k input chunks (stripes t0 .. t0+T-1, any that exist) into
  * the plane-major LDS tile by LDS-DMA: input p, plane b, stripe s at
  * ((p * 8 + b) * T + s) * 64; a wave instruction fills 1 KiB. */
-template <int T, int NW>
-__device__ __forceinline__ void stage_tile(uint8_t *lds, const uint8_t *const *base,
-                                           uint64_t stride, u32 k, uint64_t t0,
+template <int T, int NW, typename A>
+__device__ __forceinline__ void stage_tile(uint8_t *lds, A chunk, u32 k, uint64_t t0,
                                            uint64_t nstripes, u32 wave, u32 lane)
 {
+    /* chunk(p, st): address of input p's chunk of stripe st (wave-uniform p:
+     * a computed address, not an indexed pointer array, which would live in
+     * VGPRs or scratch) */
     constexpr u32 PER = T / 2;                 /* wave instructions per input */
     const u32 ni = k * PER;
     for (u32 ins = wave; ins < ni; ins += NW) {
@@ -396,7 +415,7 @@ __device__ __forceinline__ void stage_tile(uint8_t *lds, const uint8_t *const *b
         const u32 seg = el >> 2;
         const uint64_t st = t0 + seg % T;
         if (st < nstripes) {
-            const uint8_t *g = base[p] + st * stride + (seg / T) * 64u + (el & 3u) * 16u;
+            const uint8_t *g = chunk(p, st) + (seg / T) * 64u + (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
                 (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
@@ -415,32 +434,59 @@ __device__ __forceinline__ void wave_lds_sync()
 /* Write the wave's T chunks (lane (cs, cc) holds column cc of stripe cs, CW
  * dwords per plane) through its LDS slice as contiguous 16-B lane pieces:
  * chunk s goes to dst(s) + [0, 512).  dst(s) = nullptr: no stripe. */
-template <int T, int CW, bool NTS, typename D>
+/* H passes: the slice holds T / H chunks (H = 2 halves the LDS a wave
+ * needs, for the k = 16 tiles where LDS decides how many blocks fit). */
+template <int T, int CW, bool NTS, int H = 1, typename D>
 __device__ __forceinline__ void store_chunks_via_lds(uint8_t *slice, const u32 (&acc)[8][CW],
                                                      u32 cs, u32 cc, u32 lane, D dst)
 {
-    uint8_t *o = slice + cs * ECD_CHUNK + cc * (4u * CW);
+    constexpr u32 SP = T / H;                  /* chunks per pass */
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        if constexpr (CW == 1)
-            *reinterpret_cast<u32 *>(o + b * 64) = acc[b][0];
-        else
-            *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
-    }
-    wave_lds_sync();
+    for (u32 h = 0; h < (u32)H; ++h) {
+        if (H == 1 || cs / SP == h) {
+            uint8_t *o = slice + (cs % SP) * ECD_CHUNK + cc * (4u * CW);
 #pragma unroll
-    for (u32 j = 0; j < T * ECD_CHUNK / 1024; ++j) {
-        const u32 off = (j * 64 + lane) * 16;
-        uint8_t *d = dst(off / ECD_CHUNK);
-        if (d) {
-            const v4u v = *reinterpret_cast<const v4u *>(slice + off);
-            if constexpr (NTS)
-                __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(d + off % ECD_CHUNK));
-            else
-                *reinterpret_cast<v4u *>(d + off % ECD_CHUNK) = v;
+            for (int b = 0; b < 8; ++b) {
+                if constexpr (CW == 1)
+                    *reinterpret_cast<u32 *>(o + b * 64) = acc[b][0];
+                else
+                    *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+            }
         }
+        wave_lds_sync();
+#pragma unroll
+        for (u32 j = 0; j < SP * ECD_CHUNK / 1024; ++j) {
+            const u32 off = (j * 64 + lane) * 16;
+            uint8_t *d = dst(h * SP + off / ECD_CHUNK);
+            if (d) {
+                const v4u v = *reinterpret_cast<const v4u *>(slice + off);
+                if constexpr (NTS)
+                    __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(d + off % ECD_CHUNK));
+                else
+                    *reinterpret_cast<v4u *>(d + off % ECD_CHUNK) = v;
+            }
+        }
+        wave_lds_sync();
     }
-    wave_lds_sync();
+}
+
+/* One fragment row of the narrow tile. */
+template <int K, int I, int T, bool NTS, bool DIRECT, bool WOT>
+__device__ __forceinline__ void encode_tile_item(const uint8_t *col, uint8_t *slice,
+                                                           uint8_t *row, uint64_t t0,
+                                                           uint64_t nstripes, u32 cs, u32 cc,
+                                                           u32 lane)
+{
+    constexpr int CW = T / 4;
+    u32 acc[8][CW];
+    encode_tile_acc<K, I, DIRECT, CW, T>(col, acc);
+    if constexpr (WOT) {
+        store_chunks_via_lds<T, CW, NTS>(slice, acc, cs, cc, lane, [&](u32 s) {
+            return t0 + s < nstripes ? row + (t0 + s) * ECD_CHUNK : nullptr;
+        });
+    } else if (t0 + cs < nstripes) {
+        store_chunk<CW, NTS>(row + (t0 + cs) * ECD_CHUNK + cc * (4u * CW), acc);
+    }
 }
 
 template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT>
@@ -456,31 +502,23 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const uint8_t *__res
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    const uint8_t *base[K];
-#pragma unroll
-    for (int p = 0; p < K; ++p)
-        base[p] = in + (uint64_t)p * ECD_CHUNK;
-    stage_tile<T, NW>(lds, base, (uint64_t)K * ECD_CHUNK, K, t0, nstripes, wave, lane);
+    stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
+        return in + st * (uint64_t)(K * ECD_CHUNK) + p * ECD_CHUNK;
+    }, K, t0, nstripes, wave, lane);
     __syncthreads();
     const u32 cs = lane / LPS, cc = lane % LPS;
     const uint8_t *col = lds + cs * 64u + cc * (4u * CW);
     uint8_t *slice = lds + K * T * ECD_CHUNK + wave * T * ECD_CHUNK;
-    const uint64_t ost = t0 + cs;
     for (u32 r = wave; r < (u32)N; r += NW) {
         const u32 ru = __builtin_amdgcn_readfirstlane(r);
+        /* the row's fragment base by a run-time index (scalar load): with
+         * out.p[I] per branch, the compiler hoisted all N per-lane store
+         * addresses out of the loop, 2 VGPRs each (173 VGPRs at 16+4) */
+        uint8_t *row = out.p[ru];
         static_for<0, N>([&](auto I) {
-            if (ru == (u32)decltype(I)::value) {
-                u32 acc[8][CW];
-                encode_tile_acc<K, decltype(I)::value, DIRECT, CW, T>(col, acc);
-                uint8_t *row = out.p[decltype(I)::value];
-                if constexpr (WOT) {
-                    store_chunks_via_lds<T, CW, NTS>(slice, acc, cs, cc, lane, [&](u32 s) {
-                        return t0 + s < nstripes ? row + (t0 + s) * ECD_CHUNK : nullptr;
-                    });
-                } else if (ost < nstripes) {
-                    store_chunk<CW, NTS>(row + ost * ECD_CHUNK + cc * (4u * CW), acc);
-                }
-            }
+            if (ru == (u32)decltype(I)::value)
+                encode_tile_item<K, decltype(I)::value, T, NTS, DIRECT, WOT>(
+                    col, slice, row, t0, nstripes, cs, cc, lane);
         });
     }
 }
@@ -966,7 +1004,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
  * Each wave item is one output row for the 4 stripes; the multiply jumps
  * into the one-dword bodies of ec_gf8_asm.h.  WOT as in ec_encode_tile_t:
  * the row's 4 chunks leave through the wave's LDS slice in 512-B runs. */
-template <int K, int NW, bool MIXED, bool NTS, bool WOT>
+template <int K, int NW, bool MIXED, bool NTS, int WOT>
 __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
 {
     constexpr u32 T = 4;
@@ -977,15 +1015,13 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
     const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
-    const uint8_t *base[K];
-#pragma unroll
-    for (int p = 0; p < K; ++p)
-        base[p] = (u32)p < k ? a.in_base[pw.byte(a, p)] : nullptr;
-    stage_tile<T, NW>(lds, base, a.in_stride, k, t0, a.nstripes, wave, lane);
+    stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
+        return a.in_base[pw.byte(a, p)] + st * a.in_stride;
+    }, k, t0, a.nstripes, wave, lane);
     __syncthreads();
     const u32 cs = lane >> 4, cc = lane & 15u;
     const uint8_t *col = lds + cs * 64u + cc * 4u;
-    uint8_t *slice = lds + K * T * ECD_CHUNK + wave * T * ECD_CHUNK;
+    uint8_t *slice = lds + K * T * ECD_CHUNK + wave * (T / (WOT ? WOT : 1)) * ECD_CHUNK;
     const uint64_t ost = t0 + cs;
     for (u32 r = wave; r < a.rows; r += NW) {
         const u32 rw = a.kw * (1 + r);
@@ -1014,7 +1050,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
             ECGF_ASM_DISPATCH_W1(acc, y, t, c);
         }
         if constexpr (WOT) {
-            store_chunks_via_lds<T, 1, NTS>(slice, acc, cs, cc, lane, [&](u32 s) {
+            store_chunks_via_lds<T, 1, NTS, WOT>(slice, acc, cs, cc, lane, [&](u32 s) {
                 return t0 + s < a.nstripes ? a.out_base[r] + (t0 + s) * a.out_stride : nullptr;
             });
         } else if (ost < a.nstripes) {
@@ -1023,10 +1059,10 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
     }
 }
 
-template <int NW, bool WOT>
+template <int NW, int WOT>
 constexpr size_t combine_n_lds(int k)
 {
-    return (size_t)k * 4 * ECD_CHUNK + (WOT ? (size_t)NW * 4 * ECD_CHUNK : 0);
+    return (size_t)k * 4 * ECD_CHUNK + (WOT ? (size_t)NW * (4 / WOT) * ECD_CHUNK : 0);
 }
 
 /* Zero-copy variant for the host-buffer path, where every input and output

@@ -30,6 +30,39 @@ def stripe_range(rank, world, nstripes, align=1):
     return s0, s1
 
 
+def parse_cpulist(text):
+    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11} (sysfs cpulist format)."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        else:
+            cpus.add(int(part))
+    return cpus
+
+
+def bind_to_node(node, sysfs="/sys/devices/system/node"):
+    """Restrict this process (the calling thread and every thread it starts
+    afterwards: the library's copy pool, the CPU engine's callers) to the
+    CPUs of NUMA node `node` that it may already use.  Returns the CPU set
+    now in force; unchanged when the node is unknown or shares no CPU."""
+    aff = set(os.sched_getaffinity(0))
+    if node is None or node < 0:
+        return aff
+    try:
+        with open(os.path.join(sysfs, "node%d" % node, "cpulist")) as f:
+            mine = aff & parse_cpulist(f.read())
+    except OSError:
+        return aff
+    if mine and mine != aff:
+        os.sched_setaffinity(0, mine)
+        return mine
+    return aff
+
+
 class Group:
     """torch.distributed wrapper that degrades to no-ops for world == 1."""
 
@@ -77,6 +110,14 @@ class Group:
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self._dev())
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
         return bool(t.item())
+
+    def gather(self, obj):
+        """Every rank's `obj` (a small picklable value), in rank order."""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def close(self):
         if self.dist and self.dist.is_initialized():

@@ -30,7 +30,7 @@ import oracle as O  # noqa: E402  (test infrastructure)
 K, N_FRAG = 16, 20
 STRIPES = 1 << 20
 SLICE = (1 << 30)                       # bytes per 1/8 of the job
-WAYS = (2, 4, 8)
+WAYS = (1, 2, 4, 8)
 
 
 def main():

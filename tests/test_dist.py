@@ -82,3 +82,74 @@ def test_stripe_range_properties():
                 for (a0, a1), (b0, b1) in zip(rs, rs[1:]):
                     assert a1 == b0 and a0 <= a1
                     assert a1 % al == 0 or a1 == n
+
+
+def _strong_worker(rank, world, port, nstripes, q):
+    """configs[3] strong split on CPU: each rank generates ONLY its slice of
+    the one xorshift stream (synth.fill_numpy jump-ahead, the bench's
+    word0 = s0 * 512 * k / 8) and encodes it with the product's CPU engine;
+    the gathered fragments must equal the oracle's encode of the whole job."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle")]
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import oracle as O
+    import glusterfs_amd as g
+    from glusterfs_amd import synth
+    from glusterfs_amd.dist import Group, stripe_range
+
+    k, n = 16, 20
+    grp = Group(backend="gloo")
+    s0, s1 = stripe_range(grp.rank, grp.world, nstripes)
+    mine = synth.fill_numpy((s1 - s0) * 512 * k, word0=s0 * 512 * k // 8)
+    frags = [np.zeros((s1 - s0) * 512, np.uint8) for _ in range(n)]
+    with g.ECMatrixList(k, n, gen="none") as L:
+        L.encode_batch(s1 - s0, mine, frags)
+    parts = grp.gather([f.tobytes() for f in frags])
+    ok = True
+    if grp.rank == 0:
+        full = O.encode(k, n, O.fill_xorshift(nstripes * 512 * k))
+        for i in range(n):
+            cat = b"".join(p[i] for p in parts)
+            ok &= cat == full[i].tobytes()
+    ok = grp.all_ok(ok)
+    grp.close()
+    q.put((rank, ok, s0, s1))
+
+
+def test_two_rank_strong_job():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world, nst = 2, 1001
+    ps = [ctx.Process(target=_strong_worker, args=(r, world, port, nst, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] for r in res)
+    assert res[0][2] == 0 and res[0][3] == res[1][2] and res[1][3] == nst
+
+
+def test_bind_to_node(tmp_path):
+    """bench.py's rank placement: the rank keeps the CPUs of its GPU's NUMA
+    node that it may use (sysfs cpulist format), and nothing changes for an
+    unknown node or a node without usable CPUs."""
+    from glusterfs_amd.dist import bind_to_node, parse_cpulist
+    assert parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    aff = set(os.sched_getaffinity(0))
+    try:
+        assert bind_to_node(-1) == aff
+        node = tmp_path / "node0"
+        node.mkdir()
+        pick = sorted(aff)[:1]
+        (node / "cpulist").write_text("%d\n" % pick[0])
+        assert bind_to_node(0, sysfs=str(tmp_path)) == set(pick)
+        assert set(os.sched_getaffinity(0)) == set(pick)
+        (node / "cpulist").write_text("100000\n")            # no usable CPU: unchanged
+        assert bind_to_node(0, sysfs=str(tmp_path)) == set(pick)
+    finally:
+        os.sched_setaffinity(0, aff)

@@ -177,7 +177,7 @@ static void add_shipped_combine(std::vector<Variant> &v, const char *nm, const C
                  }, out, ob});
 }
 
-template <int K, int NW, bool WOT>
+template <int K, int NW, int WOT>
 static void add_combine_n(std::vector<Variant> &v, const char *nm, const CombineArgs *a,
                           double bytes, uint8_t *out, size_t ob)
 {
@@ -213,15 +213,11 @@ int main(int argc, char **argv)
         const uint64_t nst = user / (16 * ECD_CHUNK);
         FragPtrs f = frag_ptrs(bufB, nst, 20);
         add_shipped_encode(v, "shipped (tile T8 CW1 NW16)", 16, 20, nst, bufA, f);
-        add_tile_t<16, 20, 8, 10, false, false>(v, "T8 NW10", nst, bufA, f);
-        add_tile_t<16, 20, 8, 10, false, true>(v, "T8 NW10 WOT", nst, bufA, f);
-        add_tile_t<16, 20, 4, 4, false, false>(v, "T4 NW4", nst, bufA, f);
         add_tile_t<16, 20, 4, 4, false, true>(v, "T4 NW4 WOT", nst, bufA, f);
-        add_tile_t<16, 20, 4, 5, false, false>(v, "T4 NW5", nst, bufA, f);
         add_tile_t<16, 20, 4, 5, false, true>(v, "T4 NW5 WOT", nst, bufA, f);
-        add_tile_t<16, 20, 4, 10, false, false>(v, "T4 NW10", nst, bufA, f);
         add_tile_t<16, 20, 4, 10, false, true>(v, "T4 NW10 WOT", nst, bufA, f);
-        add_tile_t<16, 20, 4, 5, true, false>(v, "T4 NW5 direct", nst, bufA, f);
+        add_tile_t<16, 20, 4, 20, false, true>(v, "T4 NW20 WOT", nst, bufA, f);
+        add_tile_t<16, 20, 4, 5, true, true>(v, "T4 NW5 direct WOT", nst, bufA, f);
         run_group("encode 16+4", v, rounds, iters, s);
         v.clear();
     }
@@ -231,14 +227,12 @@ int main(int argc, char **argv)
             FragPtrs f = frag_ptrs(bufB, nst, 12);
             add_shipped_encode(v, big ? "shipped (tile T8 CW2 NW16 direct)" : "shipped (vander W1)",
                                8, 12, nst, bufA, f);
-            add_tile_t<8, 12, 8, 6, true, false>(v, "T8 NW6 direct", nst, bufA, f);
-            add_tile_t<8, 12, 8, 6, true, true>(v, "T8 NW6 direct WOT", nst, bufA, f);
             add_tile_t<8, 12, 8, 12, true, true>(v, "T8 NW12 direct WOT", nst, bufA, f);
-            add_tile_t<8, 12, 4, 4, true, false>(v, "T4 NW4 direct", nst, bufA, f);
             add_tile_t<8, 12, 4, 4, true, true>(v, "T4 NW4 direct WOT", nst, bufA, f);
             add_tile_t<8, 12, 4, 6, true, true>(v, "T4 NW6 direct WOT", nst, bufA, f);
             add_tile_t<8, 12, 4, 6, false, true>(v, "T4 NW6 WOT", nst, bufA, f);
-            add_tile_t<8, 12, 4, 12, true, true>(v, "T4 NW12 direct WOT", nst, bufA, f);
+            add_tile_t<8, 12, 4, 4, false, true>(v, "T4 NW4 WOT", nst, bufA, f);
+            add_tile_t<8, 12, 4, 12, false, true>(v, "T4 NW12 WOT", nst, bufA, f);
             run_group(big ? "encode 8+4 (size = GiB arg)" : "encode 8+4, 64K stripes", v, rounds,
                       iters, s);
             v.clear();
@@ -249,10 +243,10 @@ int main(int argc, char **argv)
         FragPtrs f = frag_ptrs(bufB, nst, 6);
         add_shipped_encode(v, "shipped (combine NW16 jt)", 4, 6, nst, bufA, f);
         add_tile_t<4, 6, 8, 6, true, true>(v, "T8 NW6 direct WOT", nst, bufA, f);
-        add_tile_t<4, 6, 8, 6, false, true>(v, "T8 NW6 WOT", nst, bufA, f);
         add_tile_t<4, 6, 4, 6, true, true>(v, "T4 NW6 direct WOT", nst, bufA, f);
+        add_tile_t<4, 6, 4, 6, false, true>(v, "T4 NW6 WOT", nst, bufA, f);
         add_tile_t<4, 6, 4, 3, true, true>(v, "T4 NW3 direct WOT", nst, bufA, f);
-        add_tile_t<4, 6, 8, 6, true, false>(v, "T8 NW6 direct", nst, bufA, f);
+        add_tile_t<4, 6, 4, 3, false, true>(v, "T4 NW3 WOT", nst, bufA, f);
         run_group("encode 4+2", v, rounds, iters, s);
         v.clear();
     }
@@ -270,11 +264,13 @@ int main(int argc, char **argv)
         const double bytes = (double)nst * (K + rows) * ECD_CHUNK;
         const size_t ob = (size_t)nst * rows * ECD_CHUNK;
         add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
-        add_combine_n<K, 8, false>(v, "narrow NW8", a, bytes, bufB, ob);
-        add_combine_n<K, 8, true>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
-        add_combine_n<K, 4, false>(v, "narrow NW4", a, bytes, bufB, ob);
-        add_combine_n<K, 4, true>(v, "narrow NW4 WOT", a, bytes, bufB, ob);
-        add_combine_n<K, 16, false>(v, "narrow NW16", a, bytes, bufB, ob);
+        add_combine_n<K, 8, 0>(v, "narrow NW8", a, bytes, bufB, ob);
+        add_combine_n<K, 8, 1>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
+        add_combine_n<K, 8, 2>(v, "narrow NW8 WOT/2", a, bytes, bufB, ob);
+        add_combine_n<K, 4, 0>(v, "narrow NW4", a, bytes, bufB, ob);
+        add_combine_n<K, 4, 1>(v, "narrow NW4 WOT", a, bytes, bufB, ob);
+        add_combine_n<K, 4, 2>(v, "narrow NW4 WOT/2", a, bytes, bufB, ob);
+        add_combine_n<K, 6, 2>(v, "narrow NW6 WOT/2", a, bytes, bufB, ob);
         run_group(title, v, rounds, iters, s);
         v.clear();
     };
@@ -286,6 +282,94 @@ int main(int argc, char **argv)
         decode_group(std::integral_constant<int, 8>{}, "heal 8+4 (4 rows)", true);
     if (want(groups, "dec4"))
         decode_group(std::integral_constant<int, 4>{}, "decode 4+2 dense", false);
+    if (want(groups, "dec8b")) {   /* configs[2]: one 64K-stripe batch, 8+4 decode */
+        constexpr int K = 8;
+        const uint64_t nst = 65536;
+        uint8_t *fr[8];
+        for (int p = 0; p < K; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        uint8_t c[64];
+        for (int i = 0; i < 64; ++i)
+            c[i] = (uint8_t)(1 + (i * 173 + 11) % 255);
+        const CombineArgs *a = make_args(K, K, nst, fr, bufB, true, c);
+        const double bytes = 2.0 * nst * K * ECD_CHUNK;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
+        add_combine_n<K, 4, 0>(v, "narrow NW4", a, bytes, bufB, ob);
+        add_combine_n<K, 4, 1>(v, "narrow NW4 WOT", a, bytes, bufB, ob);
+        add_combine_n<K, 8, 1>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
+        run_group("decode 8+4, 64K stripes", v, rounds, iters, s);
+        v.clear();
+    }
+    auto mixed_group = [&](auto kk, int n, int np, const char *title) {
+        /* np random dense patterns over n fragments, 1024-stripe groups */
+        constexpr int K = decltype(kk)::value;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        ecd_combine_desc_t d;
+        memset(&d, 0, sizeof(d));
+        d.k = K;
+        d.rows = K;
+        d.nstripes = nst;
+        d.in_stride = ECD_CHUNK;
+        d.out_stride = (uint64_t)K * ECD_CHUNK;
+        for (int f = 0; f < n; ++f)
+            d.in_base[f] = bufA + (uint64_t)f * nst * ECD_CHUNK * K / n;
+        for (int r = 0; r < K; ++r)
+            d.out_base[r] = bufB + (uint64_t)r * ECD_CHUNK;
+        d.npatterns = np;
+        d.pat_bytes = K + K * K;
+        std::vector<uint8_t> pats((size_t)np * d.pat_bytes);
+        uint32_t x = 7;
+        for (int q = 0; q < np; ++q) {
+            uint8_t *pp = pats.data() + q * d.pat_bytes;
+            int used = 0;
+            for (int f = 0; f < n && used < K; ++f) {
+                x = x * 1103515245u + 12345u;
+                if ((int)((x >> 16) % (n - f)) < K - used)
+                    pp[used++] = (uint8_t)f;
+            }
+            for (int i = 0; i < K * K; ++i) {
+                x = x * 1103515245u + 12345u;
+                pp[K + i] = (uint8_t)(1 + (x >> 16) % 255);
+            }
+        }
+        d.pat_ext = pats.data();
+        const uint64_t ngroups = (nst + 1023) / 1024;
+        std::vector<uint8_t> gp(ngroups);
+        for (auto &g : gp) {
+            x = x * 1103515245u + 12345u;
+            g = (uint8_t)((x >> 16) % np);
+        }
+        uint8_t *dgp;
+        CHK(hipMalloc(&dgp, ngroups));
+        CHK(hipMemcpy(dgp, gp.data(), ngroups, hipMemcpyHostToDevice));
+        d.group_pattern = dgp;
+        d.group_shift = 10;
+        CombineArgs *a = new CombineArgs;
+        if (ecdk_pack_args(&d, a) != 0) {
+            printf("(%s: pattern table case not covered here)\n", title);
+            return;
+        }
+        const double bytes = 2.0 * nst * K * ECD_CHUNK;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
+        auto addm = [&](const char *nm, auto kern, int nw, size_t lds) {
+            lds_attr((const void *)kern, lds);
+            const uint64_t g = (nst + 3) / 4;
+            v.push_back({nm, bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * nw), lds, st, *a);
+                         }, bufB, ob});
+        };
+        addm("narrow NW4 WOT", ec_combine_n<K, 4, true, true, 1>, 4, combine_n_lds<4, 1>(K));
+        addm("narrow NW8", ec_combine_n<K, 8, true, true, 0>, 8, combine_n_lds<8, 0>(K));
+        addm("narrow NW8 WOT/2", ec_combine_n<K, 8, true, true, 2>, 8, combine_n_lds<8, 2>(K));
+        run_group(title, v, rounds, iters, s);
+        v.clear();
+    };
+    if (want(groups, "mixed8"))
+        mixed_group(std::integral_constant<int, 8>{}, 12, 16, "mixed 8+4, 16 patterns, 1024-stripe groups");
+    if (want(groups, "mixed16"))
+        mixed_group(std::integral_constant<int, 16>{}, 20, 7, "mixed 16+4, 7 patterns, 1024-stripe groups");
     CHK(hipFree(bufA));
     CHK(hipFree(bufB));
     return 0;
