@@ -202,16 +202,40 @@ int launch_encode_42_combine(hipStream_t s, uint64_t nstripes, const void *in, v
 } // namespace
 
 /* EC_MI355X_ENC=0 keeps the register-resident encoder for every geometry,
- * =2 takes the tile encoders at every size (A/B runs only); unset = the
- * shipped choice. */
+ * =1 the round-2 choice (8-stripe tile encoders), =2 those at every size
+ * (A/B runs only); unset = the narrow-tile encoders (3). */
 static int enc_mode()
 {
     static const int v = [] {
         const char *e = getenv("EC_MI355X_ENC");
-        return e && (*e == '0' || *e == '2') ? *e - '0' : 1;
+        return e && (*e == '0' || *e == '1' || *e == '2') ? *e - '0' : 3;
     }();
     return v;
 }
+
+namespace {
+
+/* Narrow-tile encoder (ec_encode_tile_t): 4-stripe tiles, NW waves, each
+ * fragment row's 4 chunks stored as one 2 KiB run (tools/kbench/kb3.hip,
+ * profiles/kb3_r03*.log). */
+template <int K, int N, int NW, bool DIRECT>
+int launch_encode_narrow(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
+{
+    FragPtrs f;
+    for (int i = 0; i < N; ++i)
+        f.p[i] = static_cast<uint8_t *>(out[i]);
+    const uint64_t g = (nstripes + 3) / 4;
+    if (g == 0)
+        return 0;
+    if (g > 0x7fffffffull)
+        return -EINVAL;
+    hipLaunchKernelGGL((ec_encode_tile_t<K, N, 4, NW, true, DIRECT, true>), dim3((u32)g),
+                       dim3(NW * 64), (encode_tile_t_lds<4, NW, true>(K)), s,
+                       static_cast<const uint8_t *>(in), f, nstripes);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+} // namespace
 
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                        const void *in, void *const *out, bool zc)
@@ -219,7 +243,16 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
     /* the tile encoders stage their input by LDS-DMA in 16-byte pieces; an
      * input at any other alignment (a tensor slice) keeps the
      * register-resident encoder, whose loads take any byte address */
-    const bool tiles = !zc && enc_mode() != 0 && !((uintptr_t)in & 15);
+    const bool aligned = !((uintptr_t)in & 15);
+    if (!zc && aligned && enc_mode() == 3) {
+        if (k == 4 && n == 6)
+            return launch_encode_narrow<4, 6, 6, true>(s, nstripes, in, out);
+        if (k == 8 && n == 12)
+            return launch_encode_narrow<8, 12, 6, false>(s, nstripes, in, out);
+        if (k == 16 && n == 20)
+            return launch_encode_narrow<16, 20, 4, false>(s, nstripes, in, out);
+    }
+    const bool tiles = !zc && enc_mode() != 0 && aligned;
     if (tiles && k == 4 && n == 6)
         return launch_encode_42_combine(s, nstripes, in, out);
     if (tiles && k == 8 && n == 12 && (nstripes > (1u << 17) || enc_mode() == 2))
@@ -550,8 +583,32 @@ int nw16_override()
 /* Pattern groups of 1, 2 or 4 stripes: sort the stripes by pattern into
  * 8-slot tiles (ec_slots_*, ec_kernels_impl.h) and run the tile kernel over
  * the slot list.  Workspace: stream-ordered, freed after the launch. */
+template <bool NTS, typename F>
+int sorted_slots(hipStream_t s, const CombineArgs &a0, F tiles);
+
 template <bool NTS>
 int launch_combine_slots(hipStream_t s, const CombineArgs &a0)
+{
+    return sorted_slots<NTS>(s, a0, [](hipStream_t st, const CombineArgs &a) {
+        /* waves per block: 4 for k <= 4 (1-/4-stripe groups of 4+2 0.49 ->
+         * 0.45 ms per GiB against 8), 8 for k <= 8 (4 and 16 slower), same
+         * box through this launcher (profiles/ab_slots_r02z.log) */
+        if (a.k <= 4)
+            return nw4_override() == 16  ? launch_combine<4, 1, 16, 16, NTS, 1, 1, true>(st, a)
+                   : nw4_override() == 8 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, true>(st, a)
+                                         : launch_combine<4, 1, 4, 4, NTS, 1, 1, true>(st, a);
+        if (a.k <= 8)
+            return nw8_override() == 16  ? launch_combine<8, 1, 16, 16, NTS, 1, 1, true>(st, a)
+                   : nw8_override() == 4 ? launch_combine<8, 1, 4, 4, NTS, 1, 1, true>(st, a)
+                                         : launch_combine<8, 1, 8, 8, NTS, 1, 1, true>(st, a);
+        return launch_combine<16, 1, 16, 16, NTS, 1, 1, true>(st, a);
+    });
+}
+
+/* Pattern groups below one tile: sort the stripes by pattern into slot
+ * runs padded to 8 (ec_slots_*), then tiles(stream, args-with-slots). */
+template <bool NTS, typename F>
+int sorted_slots(hipStream_t s, const CombineArgs &a0, F tiles)
 {
     if (a0.nstripes == 0)
         return 0;
@@ -580,21 +637,8 @@ int launch_combine_slots(hipStream_t s, const CombineArgs &a0)
                            slots);
         rc = hipGetLastError() == hipSuccess ? 0 : -EIO;
     }
-    if (rc == 0) {
-        /* waves per block: 4 for k <= 4 (1-/4-stripe groups of 4+2 0.49 ->
-         * 0.45 ms per GiB against 8), 8 for k <= 8 (4 and 16 slower), same
-         * box through this launcher (profiles/ab_slots_r02z.log) */
-        if (a.k <= 4)
-            rc = nw4_override() == 16  ? launch_combine<4, 1, 16, 16, NTS, 1, 1, true>(s, a)
-                 : nw4_override() == 8 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, true>(s, a)
-                                       : launch_combine<4, 1, 4, 4, NTS, 1, 1, true>(s, a);
-        else if (a.k <= 8)
-            rc = nw8_override() == 16  ? launch_combine<8, 1, 16, 16, NTS, 1, 1, true>(s, a)
-                 : nw8_override() == 4 ? launch_combine<8, 1, 4, 4, NTS, 1, 1, true>(s, a)
-                                       : launch_combine<8, 1, 8, 8, NTS, 1, 1, true>(s, a);
-        else
-            rc = launch_combine<16, 1, 16, 16, NTS, 1, 1, true>(s, a);
-    }
+    if (rc == 0)
+        rc = tiles(s, a);
     (void)hipFreeAsync(ws, s);
     return rc;
 }
@@ -657,8 +701,73 @@ int output_tile_mode(const CombineArgs &a)
     return 1;
 }
 
+/* ------------------------------------------------ narrow tiles (r03) */
+
+/* EC_MI355X_NARROW=0 restores the 8-stripe ec_combine for every device
+ * combination (A/B runs); unset = the narrow-tile kernels. */
+bool narrow_on()
+{
+    static const bool v = [] {
+        const char *e = getenv("EC_MI355X_NARROW");
+        return !(e && *e == '0');
+    }();
+    return v;
+}
+
+template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG, bool SL>
+int launch_n1(hipStream_t s, const CombineArgs &a, uint64_t g)
+{
+    if (g == 0)
+        return 0;
+    if (g > 0x7fffffffull)
+        return -EINVAL;
+    const size_t lds = combine_n_lds<NW, WOT, PG>((int)a.k);
+    hipLaunchKernelGGL((ec_combine_n<K, NW, MIXED, NTS, WOT, PG, SL>), dim3((u32)g),
+                       dim3(NW * 64), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+/* one k-bucket: single pattern, mixed, device pattern table, sorted slots */
+template <int K, int NW, int WOT, bool NTS>
+int launch_narrow_k(hipStream_t s, const CombineArgs &a)
+{
+    if (!a.group_pattern)
+        return launch_n1<K, NW, false, NTS, WOT, false, false>(s, a, (a.nstripes + 3) / 4);
+    if (a.group_shift >= 2)          /* groups of >= 4 stripes: a tile is one pattern's */
+        return a.patg ? launch_n1<K, NW, true, NTS, WOT, true, false>(s, a, (a.nstripes + 3) / 4)
+                      : launch_n1<K, NW, true, NTS, WOT, false, false>(s, a, (a.nstripes + 3) / 4);
+    return sorted_slots<NTS>(s, a, [](hipStream_t st, const CombineArgs &b) {
+        /* runs padded to multiples of 8 slots: worst case 7 per pattern */
+        const uint64_t g = (b.nstripes + 8ull * b.npatterns) / 4 + 1;
+        return b.patg ? launch_n1<K, NW, true, NTS, WOT, true, true>(st, b, g)
+                      : launch_n1<K, NW, true, NTS, WOT, false, true>(st, b, g);
+    });
+}
+
+/* Waves per block and output staging per k (tools/kbench/kb3.hip, one
+ * process, 7 interleaved rounds; profiles/kb3_r03*.log). */
+template <bool NTS>
+int launch_narrow(hipStream_t s, const CombineArgs &a)
+{
+    if (a.k <= 4)
+        return launch_narrow_k<4, 4, 1, NTS>(s, a);
+    if (a.k <= 8)
+        return launch_narrow_k<8, 4, 1, NTS>(s, a);
+    return launch_narrow_k<16, 8, 0, NTS>(s, a);
+}
+
+template <bool NTS>
+int launch_combine_r02(hipStream_t s, const CombineArgs &a);
+
 template <bool NTS>
 int launch_combine_k(hipStream_t s, const CombineArgs &a)
+{
+    return narrow_on() ? launch_narrow<NTS>(s, a) : launch_combine_r02<NTS>(s, a);
+}
+
+/* Round 2's 8-stripe ec_combine dispatch (EC_MI355X_NARROW=0, A/B). */
+template <bool NTS>
+int launch_combine_r02(hipStream_t s, const CombineArgs &a)
 {
     const int jt = jt_override();
     if (a.k <= 4 && jt != 0 && !(a.group_pattern && a.group_shift < 3)) {

@@ -404,9 +404,9 @@ template <int T, int NW, typename A>
 __device__ __forceinline__ void stage_tile(uint8_t *lds, A chunk, u32 k, uint64_t t0,
                                            uint64_t nstripes, u32 wave, u32 lane)
 {
-    /* chunk(p, st): address of input p's chunk of stripe st (wave-uniform p:
-     * a computed address, not an indexed pointer array, which would live in
-     * VGPRs or scratch) */
+    /* chunk(p, st): address of input p's chunk of stripe st, nullptr for
+     * none (a padding slot); p is wave-uniform -- a computed address, not an
+     * indexed pointer array, which would live in VGPRs or scratch */
     constexpr u32 PER = T / 2;                 /* wave instructions per input */
     const u32 ni = k * PER;
     for (u32 ins = wave; ins < ni; ins += NW) {
@@ -414,8 +414,9 @@ __device__ __forceinline__ void stage_tile(uint8_t *lds, A chunk, u32 k, uint64_
         const u32 el = (ins % PER) * 64 + lane;  /* 16-B piece within input p */
         const u32 seg = el >> 2;
         const uint64_t st = t0 + seg % T;
-        if (st < nstripes) {
-            const uint8_t *g = chunk(p, st) + (seg / T) * 64u + (el & 3u) * 16u;
+        const uint8_t *c = st < nstripes ? chunk(p, st) : nullptr;
+        if (c) {
+            const uint8_t *g = c + (seg / T) * 64u + (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
                 (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
@@ -1003,8 +1004,10 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
  * stripe), so a k = 16 tile is 32 KiB and four 8-wave blocks share a CU.
  * Each wave item is one output row for the 4 stripes; the multiply jumps
  * into the one-dword bodies of ec_gf8_asm.h.  WOT as in ec_encode_tile_t:
- * the row's 4 chunks leave through the wave's LDS slice in 512-B runs. */
-template <int K, int NW, bool MIXED, bool NTS, int WOT>
+ * the row's 4 chunks leave through the wave's LDS slice in 512-B runs (WOT
+ * = 2: a half slice, two passes).  PG and SLOTS as in ec_combine (device
+ * pattern table; sorted slots, whose runs are padded to 8 and so to 4). */
+template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG = false, bool SLOTS = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
 {
     constexpr u32 T = 4;
@@ -1014,15 +1017,26 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
-    stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
-        return a.in_base[pw.byte(a, p)] + st * a.in_stride;
-    }, k, t0, a.nstripes, wave, lane);
+    u32 nslots = 0;
+    if constexpr (SLOTS) {
+        nslots = __builtin_amdgcn_readfirstlane(*a.slot_count);
+        if (t0 >= nslots)
+            return;             /* the grid is sized for the worst padding */
+    }
+    const uint64_t tp = SLOTS ? slot_stripe<SLOTS>(a, t0, nslots) : t0;
+    constexpr u32 SLICE = WOT ? (T / WOT) * ECD_CHUNK : 0;
+    /* LDS: the k-input tile, NW output slices, then (PG) the pattern */
+    const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp), lane,
+                          lds + k * T * ECD_CHUNK + NW * SLICE);
+    stage_tile<T, NW>(lds, [&](u32 p, uint64_t slot) -> const uint8_t * {
+        const uint64_t st = slot_stripe<SLOTS>(a, slot, nslots);
+        return st != kNoSlot ? a.in_base[pw.byte(a, p)] + st * a.in_stride : nullptr;
+    }, k, t0, SLOTS ? (uint64_t)nslots : a.nstripes, wave, lane);
     __syncthreads();
     const u32 cs = lane >> 4, cc = lane & 15u;
     const uint8_t *col = lds + cs * 64u + cc * 4u;
-    uint8_t *slice = lds + K * T * ECD_CHUNK + wave * (T / (WOT ? WOT : 1)) * ECD_CHUNK;
-    const uint64_t ost = t0 + cs;
+    uint8_t *slice = lds + k * T * ECD_CHUNK + wave * SLICE;
+    const uint64_t ost = slot_stripe<SLOTS>(a, t0 + cs, nslots);
     for (u32 r = wave; r < a.rows; r += NW) {
         const u32 rw = a.kw * (1 + r);
         const u32 w0 = pw.word(a, rw);
@@ -1051,18 +1065,21 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
         }
         if constexpr (WOT) {
             store_chunks_via_lds<T, 1, NTS, WOT>(slice, acc, cs, cc, lane, [&](u32 s) {
-                return t0 + s < a.nstripes ? a.out_base[r] + (t0 + s) * a.out_stride : nullptr;
+                const uint64_t o = s == cs ? ost : slot_stripe<SLOTS>(a, t0 + s, nslots);
+                return o != kNoSlot ? a.out_base[r] + o * a.out_stride : nullptr;
             });
-        } else if (ost < a.nstripes) {
+        } else if (ost != kNoSlot) {
             store_chunk<1, NTS>(a.out_base[r] + ost * a.out_stride + cc * 4u, acc);
         }
     }
 }
 
-template <int NW, int WOT>
+/* dynamic LDS of an ec_combine_n launch for k inputs */
+template <int NW, int WOT, bool PG = false>
 constexpr size_t combine_n_lds(int k)
 {
-    return (size_t)k * 4 * ECD_CHUNK + (WOT ? (size_t)NW * (4 / WOT) * ECD_CHUNK : 0);
+    return (size_t)k * 4 * ECD_CHUNK + (WOT ? (size_t)NW * (4 / WOT) * ECD_CHUNK : 0) +
+           (PG ? kPatLdsBytes : 0);
 }
 
 /* Zero-copy variant for the host-buffer path, where every input and output

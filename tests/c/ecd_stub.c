@@ -37,3 +37,5 @@ int ecd_host_unregister(void *p) { (void)p; return -ENODEV; }
 uint64_t ecd_host_inflight(void) { return UINT64_MAX; }
 void ecd_inject_faults(uint32_t n) { (void)n; }
 int ecd_host_mapped(const void *p, size_t n) { (void)p; (void)n; return 0; }
+int ecd_device_numa_node(int d) { (void)d; return -ENODEV; }
+int ecd_copy_threads(void) { return 0; }
