@@ -668,7 +668,17 @@ def cpu_baseline(budget_s=4.0):
     throttled = cpu_stat_delta(t0)
     enc_1, _ = _rate(lambda: O.encode(k, n, data, nthreads=1, out=frags), S, 0.5)
     dec_1, _ = _rate(lambda: O.decode(k, rows, ins, nthreads=1, out=out), S, 0.5)
+    # the reference's default engine is the AVX JIT (ec-code-avx.c); it is
+    # not buildable here, so its rate is estimated from this oracle by the
+    # one-thread ratio of the survey session's compiled-reference avx figures
+    # (4.4 / 6.1-6.4 GB/s) to this oracle in the build
+    # container (2.96 / 3.99 GB/s) -- an estimate, not a run
+    cal = dict(encode=1.49, decode=1.57)
     return dict(value=dec_T, unit="GB/s", cores=T, kind="port", threads=T,
+                reference_avx_estimate=dict(
+                    decode_GBps=round(dec_T * cal["decode"], 2),
+                    encode_1GiB_GBps=round(enc_T * cal["encode"], 2),
+                    calibration=cal, how="oracle rate x (reference avx / oracle, one thread)"),
                 nproc=hc["nproc"], affinity_cpus=hc["affinity"],
                 cgroup_cpu_quota=hc["cgroup_quota"], model=hc["model"],
                 encode_1GiB_GBps=enc_T, one_thread_encode_GBps=enc_1,

@@ -244,13 +244,17 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
      * input at any other alignment (a tensor slice) keeps the
      * register-resident encoder, whose loads take any byte address */
     const bool aligned = !((uintptr_t)in & 15);
+    /* narrow-tile encoders, same A/B (ms per GiB unless noted): 4+2 0.438 ->
+     * 0.423 (6 waves, direct products), 8+4 0.443 -> 0.411 and 64K-stripe
+     * batches 0.126 -> 0.095 ms (12 waves, Horner: one row per wave, and the
+     * 2 KiB row runs remove the 64-B segment writes of the register
+     * encoder, PMC 1.10x); 16+4 keeps the 8-stripe tile encoder (0.432
+     * against 0.453) */
     if (!zc && aligned && enc_mode() == 3) {
         if (k == 4 && n == 6)
             return launch_encode_narrow<4, 6, 6, true>(s, nstripes, in, out);
         if (k == 8 && n == 12)
-            return launch_encode_narrow<8, 12, 6, false>(s, nstripes, in, out);
-        if (k == 16 && n == 20)
-            return launch_encode_narrow<16, 20, 4, false>(s, nstripes, in, out);
+            return launch_encode_narrow<8, 12, 12, false>(s, nstripes, in, out);
     }
     const bool tiles = !zc && enc_mode() != 0 && aligned;
     if (tiles && k == 4 && n == 6)
@@ -744,25 +748,33 @@ int launch_narrow_k(hipStream_t s, const CombineArgs &a)
     });
 }
 
-/* Waves per block and output staging per k (tools/kbench/kb3.hip, one
- * process, 7 interleaved rounds; profiles/kb3_r03*.log). */
+template <bool NTS>
+int launch_combine_r02(hipStream_t s, const CombineArgs &a);
+
+/* The device combine for k <= 8: narrow tiles with per-wave output staging
+ * (tools/kbench/kb3.hip, one process, 7 interleaved rounds against the
+ * round-2 dispatch, profiles/kb3_r03d.log, ms per GiB unless noted):
+ *   4+2 decode (dense)      0.366 -> 0.350   4 waves
+ *   8+4 decode              0.371 -> 0.350   4 waves
+ *   8+4 decode, 64K stripes 0.096 -> 0.083   8 waves (small batches)
+ *   8+4 heal (4 rows)       0.316 -> 0.263   4 waves
+ *   8+4 mixed, 16 masks     0.395 -> 0.375   4 waves
+ * k = 16 keeps the 8-stripe ec_combine: 16+4 decode 0.406 against 0.421 at
+ * best narrow (8 waves, register stores), mixed 0.395 against 0.442. */
 template <bool NTS>
 int launch_narrow(hipStream_t s, const CombineArgs &a)
 {
     if (a.k <= 4)
         return launch_narrow_k<4, 4, 1, NTS>(s, a);
-    if (a.k <= 8)
-        return launch_narrow_k<8, 4, 1, NTS>(s, a);
-    return launch_narrow_k<16, 8, 0, NTS>(s, a);
+    if (a.nstripes <= (1u << 17))
+        return launch_narrow_k<8, 8, 1, NTS>(s, a);
+    return launch_narrow_k<8, 4, 1, NTS>(s, a);
 }
-
-template <bool NTS>
-int launch_combine_r02(hipStream_t s, const CombineArgs &a);
 
 template <bool NTS>
 int launch_combine_k(hipStream_t s, const CombineArgs &a)
 {
-    return narrow_on() ? launch_narrow<NTS>(s, a) : launch_combine_r02<NTS>(s, a);
+    return narrow_on() && a.k <= 8 ? launch_narrow<NTS>(s, a) : launch_combine_r02<NTS>(s, a);
 }
 
 /* Round 2's 8-stripe ec_combine dispatch (EC_MI355X_NARROW=0, A/B). */

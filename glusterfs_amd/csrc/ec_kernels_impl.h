@@ -1023,7 +1023,12 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
         if (t0 >= nslots)
             return;             /* the grid is sized for the worst padding */
     }
+    /* a sorted tile is one pattern's: take it from the tile's first slot.
+     * Runs are padded to 8 slots, so a 4-slot tile can be all padding
+     * (a run of 1-3 stripes): nothing to do, and no pattern to look up */
     const uint64_t tp = SLOTS ? slot_stripe<SLOTS>(a, t0, nslots) : t0;
+    if (SLOTS && tp == kNoSlot)
+        return;
     constexpr u32 SLICE = WOT ? (T / WOT) * ECD_CHUNK : 0;
     /* LDS: the k-input tile, NW output slices, then (PG) the pattern */
     const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp), lane,
