@@ -29,6 +29,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/ec_method.h"
 #include "ec_cpu.h"
@@ -326,6 +327,7 @@ env_u64(const char *name, uint64_t dflt)
 
 static struct {
     uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, page_gbps_l, always;
+    uint64_t adapt;
 } __attribute__((aligned(64))) ecm_x;
 static pthread_once_t ecm_xover_once __attribute__((aligned(64))) = PTHREAD_ONCE_INIT;
 
@@ -341,6 +343,7 @@ xover_init(void)
     ecm_x.page_gbps = env_u64("EC_GPU_PAGEABLE_GBPS", 14);
     ecm_x.page_gbps_l = env_u64("EC_GPU_PAGEABLE_GBPS_L", 21);
     ecm_x.always = env_u64("EC_GPU_ALWAYS", 0);
+    ecm_x.adapt = env_u64("EC_XOVER_ADAPT", 1);
 }
 
 enum { ECM_ENCODE = 0, ECM_DECODE = 1 };
@@ -348,11 +351,81 @@ enum { ECM_ENCODE = 0, ECM_DECODE = 1 };
 /* 1: code this host-buffer call on the CPU engine.  `user`: user bytes of
  * the call; `moved`: bytes read + written; `op`: ECM_ENCODE / ECM_DECODE;
  * `mapped`: every buffer is pinned, device-mapped host memory. */
+/* Observed rates (r03).  The constants above are calibrated on calls that
+ * re-code cache-resident buffers; a self-heal sweep streams through a file
+ * (ec-heal.c:2048-2107), and there the CPU engine ran at a fraction of its
+ * modelled rate while the GPU with registered buffers ran 1.9x faster
+ * (bench.py heal_sweep, profiles/r03*_bench.log).  So every host call of
+ * >= 256 KiB of user data records the user-byte rate it achieved -- per
+ * engine (CPU; GPU on mapped buffers; GPU on pageable buffers), direction
+ * and code width -- as an exponential average (1/8), and once an engine has
+ * samples its observed rate replaces the model in the comparison.  An
+ * engine the router keeps losing to is re-sampled by one call of >= 1 MiB
+ * in every 64 (exploration), so a change in load or residency is noticed.
+ * EC_XOVER_ADAPT=0 keeps the static model. */
+enum { ECM_OBS_CPU = 0, ECM_OBS_GPU_MAPPED = 1, ECM_OBS_GPU_PAGEABLE = 2 };
+#define ECM_OBS_MIN (256u << 10)
+#define ECM_OBS_EXPLORE (1u << 20)
+
+static struct {
+    uint64_t kbps;   /* user KB per second, EWMA; 0: no sample yet */
+    uint32_t lost;   /* calls routed away from this engine since its last sample */
+    uint32_t pad[13];
+} __attribute__((aligned(64))) ecm_obs[3][2][3];
+
+static int
+kbucket(uint32_t k)
+{
+    return k <= 4 ? 0 : k <= 8 ? 1 : 2;
+}
+
+static uint64_t
+now_ns(void)
+{
+    struct timespec ts;
+
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+static void
+obs_record(int eng, int op, uint32_t k, uint64_t user, uint64_t ns)
+{
+    uint64_t *slot = &ecm_obs[eng][op][kbucket(k)].kbps;
+    uint64_t old, upd, sample;
+
+    if (user < ECM_OBS_MIN || ns == 0 || !ecm_x.adapt)
+        return;
+    sample = user * 1000000ull / ns;                   /* KB/s = B/ns * 1e6 / 1e3 */
+    old = __atomic_load_n(slot, __ATOMIC_RELAXED);
+    do
+        upd = old ? old + ((int64_t)sample - (int64_t)old) / 8 : sample;
+    while (!__atomic_compare_exchange_n(slot, &old, upd, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED));
+    __atomic_store_n(&ecm_obs[eng][op][kbucket(k)].lost, 0, __ATOMIC_RELAXED);
+}
+
+static double
+obs_gbps(int eng, int op, uint32_t k)
+{
+    return (double)__atomic_load_n(&ecm_obs[eng][op][kbucket(k)].kbps, __ATOMIC_RELAXED) / 1e6;
+}
+
+/* 1: send this call to the engine the router did not pick, to re-sample it */
+static int
+obs_explore(int eng, int op, uint32_t k, uint64_t user)
+{
+    uint32_t *lost = &ecm_obs[eng][op][kbucket(k)].lost;
+
+    if (!ecm_x.adapt || user < ECM_OBS_EXPLORE)
+        return 0;
+    return __atomic_add_fetch(lost, 1, __ATOMIC_RELAXED) % 64 == 0;
+}
+
 static int
 route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int mapped)
 {
     static const double isa_f[] = {0.4, 0.7, 1.0};
-    double cpu_gbps, cpu_us, gpu_us, q;
+    double cpu_gbps, cpu_us, gpu_us, q, obs;
     uint64_t infl;
 
     if (ctx->engine == ECM_ENGINE_CPU)
@@ -367,17 +440,55 @@ route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int mappe
                isa_f[ctx->isa < 0 ? 0 : ctx->isa > 2 ? 2 : ctx->isa];
     if (moved >= (32u << 20))
         cpu_gbps = cpu_gbps < 24.0 ? cpu_gbps : 24.0;
+    if (user >= ECM_OBS_MIN && (obs = obs_gbps(ECM_OBS_CPU, op, ctx->k)) > 0)
+        cpu_gbps = obs;
     cpu_us = (double)user / (cpu_gbps * 1e3);
     infl = ecd_host_inflight();
     if (infl == UINT64_MAX)
         return 1;
     q = (double)infl * ((double)user / (double)moved); /* queued user bytes */
-    gpu_us = mapped ? (double)ecm_x.pin_us + (q + user) / ((double)ecm_x.pin_gbps * 1e3)
-                    : (double)ecm_x.page_us +
-                          (q + user) / ((double)(user >= (8u << 20) ? ecm_x.page_gbps_l
-                                                                    : ecm_x.page_gbps) *
-                                        1e3);
+    obs = user >= ECM_OBS_MIN
+              ? obs_gbps(mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, op, ctx->k)
+              : 0;
+    if (obs > 0)            /* the observed rate includes the call's latency */
+        gpu_us = (q + user) / (obs * 1e3);
+    else
+        gpu_us = mapped ? (double)ecm_x.pin_us + (q + user) / ((double)ecm_x.pin_gbps * 1e3)
+                        : (double)ecm_x.page_us +
+                              (q + user) / ((double)(user >= (8u << 20) ? ecm_x.page_gbps_l
+                                                                        : ecm_x.page_gbps) *
+                                            1e3);
     return cpu_us <= gpu_us;
+}
+
+/* The engine for a host call: 1 = GPU.  `*mapped` (in: -1 unknown) is
+ * filled in when the placement had to be queried. */
+static int
+route_gpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op,
+          int (*is_mapped)(const void *), const void *arg, int *mapped)
+{
+    int gpu = 0;
+
+    /* the pinned-buffer GPU estimate is the optimistic one: a call that the
+     * CPU wins against it skips the pointer queries (which serialise in the
+     * HIP runtime: ~11 us each with 16 calling threads, tools/kbench/ptrq) */
+    if (!route_cpu(ctx, user, moved, op, 1)) {
+        *mapped = is_mapped(arg);
+        gpu = !route_cpu(ctx, user, moved, op, *mapped);
+    }
+    if (ctx->engine == ECM_ENGINE_CPU || ecm_x.always || moved < ecm_x.cpu_below)
+        return gpu;
+    if (gpu) {
+        if (obs_explore(ECM_OBS_CPU, op, ctx->k, user))
+            gpu = 0;
+    } else {
+        if (*mapped < 0 && user >= ECM_OBS_EXPLORE)
+            *mapped = is_mapped(arg);
+        if (*mapped >= 0 &&
+            obs_explore(*mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, op, ctx->k, user))
+            gpu = 1;
+    }
+    return gpu;
 }
 
 /* 1 when every non-NULL buffer of b[0..n) (len bytes each) is pinned,
@@ -877,30 +988,69 @@ popcount_mask(uintptr_t m)
 
 /* Host-buffer encode: the GPU pipeline, or the CPU engine (crossover,
  * CPU-only volumes, and the fallback when the device submission fails). */
+struct enc_bufs {
+    const void *in;
+    void *const *out;
+    uint32_t k, n;
+    uint64_t fl;
+};
+
+static int
+enc_mapped(const void *arg)
+{
+    const struct enc_bufs *b = (const struct enc_bufs *)arg;
+
+    return ecd_host_mapped(b->in, b->fl * b->k) &&
+           all_mapped((const void *const *)b->out, b->n, b->fl);
+}
+
 static int
 host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
 {
-    const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n);
-    int rc;
+    const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE, user = fl * ctx->k;
+    const uint64_t bytes = fl * (ctx->k + ctx->n);
+    const struct enc_bufs eb = {in, out, ctx->k, ctx->n, fl};
+    int rc, mapped = -1;
+    uint64_t t0;
 
-    /* the pinned-buffer GPU estimate is the optimistic one: a call that the
-     * CPU wins against it skips the pointer queries (which serialise in the
-     * HIP runtime: ~11 us each with 16 calling threads, tools/kbench/ptrq) */
-    if (!route_cpu(ctx, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k, bytes, ECM_ENCODE, 1) &&
-        !route_cpu(ctx, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k, bytes, ECM_ENCODE,
-                   ecd_host_mapped(in, nstripes * EC_METHOD_CHUNK_SIZE * ctx->k) &&
-                       all_mapped((const void *const *)out, ctx->n,
-                                  nstripes * EC_METHOD_CHUNK_SIZE))) {
+    if (route_gpu(ctx, user, bytes, ECM_ENCODE, enc_mapped, &eb, &mapped)) {
+        t0 = now_ns();
         rc = ecd_encode_host(0, ctx->k, ctx->n, nstripes, in, out, ctx->enc_pat);
         if (!gpu_failed(rc)) {
-            if (rc == 0)
+            if (rc == 0) {
                 stat_add(ECM_STAT_GPU);
+                if (mapped >= 0)
+                    obs_record(mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, ECM_ENCODE,
+                               ctx->k, user, now_ns() - t0);
+            }
             return rc;
         }
     }
+    t0 = now_ns();
     ecc_encode(ctx->isa, ctx->k, ctx->n, nstripes, (const uint8_t *)in, (uint8_t *const *)out);
+    if (ctx->engine != ECM_ENGINE_CPU)
+        obs_record(ECM_OBS_CPU, ECM_ENCODE, ctx->k, user, now_ns() - t0);
     stat_add(ECM_STAT_CPU);
     return 0;
+}
+
+struct dec_bufs {
+    const void *const *frags;
+    uint32_t nfrags;
+    void *out;
+    void *const *outs;
+    uint32_t rows;
+    uint64_t fl;
+};
+
+static int
+dec_mapped(const void *arg)
+{
+    const struct dec_bufs *b = (const struct dec_bufs *)arg;
+
+    return all_mapped(b->frags, b->nfrags, b->fl) &&
+           (b->outs ? all_mapped((const void *const *)b->outs, b->rows, b->fl)
+                    : ecd_host_mapped(b->out, b->fl * b->rows));
 }
 
 /* Host-buffer combination (decode, mixed decode, heal): the GPU pipeline or
@@ -912,23 +1062,27 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
 {
     const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (k + rows);
     const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE;
+    const struct dec_bufs db = {frags, nfrags, out, outs, rows, fl};
     ecd_combine_desc_t d;
     uint32_t f, r;
-    int rc;
+    int rc, mapped = -1;
+    uint64_t t0;
 
-    if (!route_cpu(ctx, fl * k, bytes, ECM_DECODE, 1) &&
-        !route_cpu(ctx, fl * k, bytes, ECM_DECODE,
-                   all_mapped(frags, nfrags, fl) &&
-                       (outs ? all_mapped((const void *const *)outs, rows, fl)
-                             : ecd_host_mapped(out, fl * rows)))) {
+    if (route_gpu(ctx, fl * k, bytes, ECM_DECODE, dec_mapped, &db, &mapped)) {
+        t0 = now_ns();
         rc = ecd_decode_host(0, k, rows, nstripes, nfrags, frags, out, outs, npat, pats, gp,
                              shift);
         if (!gpu_failed(rc)) {
-            if (rc == 0)
+            if (rc == 0) {
                 stat_add(ECM_STAT_GPU);
+                if (mapped >= 0)
+                    obs_record(mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, ECM_DECODE,
+                               k, fl * k, now_ns() - t0);
+            }
             return rc;
         }
     }
+    t0 = now_ns();
     memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
     d.k = k;
     d.rows = rows;
@@ -951,8 +1105,11 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
     d.group_pattern = gp;
     d.group_shift = shift;
     rc = ecc_combine(ctx->isa, &d);
-    if (rc == 0)
+    if (rc == 0) {
+        if (ctx->engine != ECM_ENGINE_CPU)
+            obs_record(ECM_OBS_CPU, ECM_DECODE, k, fl * k, now_ns() - t0);
         stat_add(ECM_STAT_CPU);
+    }
     return rc;
 }
 

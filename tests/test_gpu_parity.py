@@ -557,3 +557,34 @@ def test_decode_mixed_group_larger_than_call(ec, oracle):
     with ec.ECMatrixList(k, n) as L:
         L.decode_mixed(nst, 1 << 20, [0xF0 >> 2], frags, out)
     assert np.array_equal(out, data)
+
+
+@pytest.mark.parametrize("k,n,group", [(4, 6, 1), (4, 6, 2), (8, 12, 1), (8, 12, 2), (3, 5, 1)])
+def test_decode_mixed_short_runs(ec, oracle, k, n, group):
+    """Sorted-slot runs of 1-3 stripes: each pattern's run is padded to 8
+    slots and the narrow kernels take 4-slot tiles, so whole tiles are
+    padding (round 3: they looked their pattern up at slot ~0 and faulted).
+    Every mask appears 1-3 times; checked group by group against the
+    oracle's inverse."""
+    import torch
+    nmasks = 15
+    pool = _distinct_masks(n, k, nmasks, seed=group * 7 + k)
+    ids = []
+    rng = np.random.default_rng(k + group)
+    for m in range(nmasks):
+        ids += [m] * int(rng.integers(1, 4))
+    rng.shuffle(ids)
+    ngroups = len(ids)
+    nst = group * ngroups
+    frags = [rand_bytes(CHUNK * nst, seed=500 + f) for f in range(n)]
+    masks = [pool[i] for i in ids]
+    out = np.zeros(CHUNK * k * nst, np.uint8)
+    with ec.ECMatrixList(k, n) as L:
+        L.decode_mixed(nst, group, masks, frags, out)
+        _check_groups(oracle, k, group, nst, masks, frags, out)
+        dfr = [torch.from_numpy(f).cuda() for f in frags]
+        gp = torch.tensor(ids, dtype=torch.uint8, device="cuda")
+        dout = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+        L.decode_mixed_device(0, None, nst, group, gp, pool, dfr, dout)
+        ec.sync_device(0)
+        _check_groups(oracle, k, group, nst, masks, frags, dout.cpu().numpy())
