@@ -19,7 +19,6 @@
 #include <stdint.h>
 
 #include "ec_gf8_asm.h"
-#include "ec_gf8_asm_t4.h"
 #include "ec_gf8_prog.h"
 
 namespace ecgf {
@@ -191,23 +190,15 @@ __device__ __forceinline__ void mul_xor_rt(u32 c, u32 (&acc)[8][W], const u32 (&
  * per lane: a jump through a PC-relative table into the searched program
  * for c (ec_gf8_asm.h, generated).  Replaces the switch above where the
  * compare tree's scalar work bounds the kernel. */
-template <int W, int ALIGN = 0>
+template <int W>
 __device__ __forceinline__ void mul_xor_jt(u32 c, u32 (&acc)[8][W], const u32 (&x)[8][W])
 {
-    static_assert(W == 2, "the assembly bodies are generated for 2 dwords per lane");
-    u32 t[ECGF_ASM_TEMPS][2];
-    if constexpr (ALIGN)
-        ECGF_ASM_DISPATCH_W2_A32(acc, x, t, c);  /* bodies on 32-byte boundaries */
-    else
+    static_assert(W == 1 || W == 2, "the assembly bodies are generated for 1 or 2 dwords");
+    u32 t[ECGF_ASM_TEMPS][W];
+    if constexpr (W == 2)
         ECGF_ASM_DISPATCH_W2(acc, x, t, c);
-}
-
-/* The same with the <= 4-temporary programs of ec_gf8_asm_t4.h (8 VGPRs of
- * temporaries instead of 12: room for a second input buffer). */
-__device__ __forceinline__ void mul_xor_jt4(u32 c, u32 (&acc)[8][2], const u32 (&x)[8][2])
-{
-    u32 t[ECGF_ASM_TEMPS_T4][2];
-    ECGF_ASM_DISPATCH_W2_T4(acc, x, t, c);
+    else
+        ECGF_ASM_DISPATCH_W1(acc, x, t, c);
 }
 
 } // namespace ecgf

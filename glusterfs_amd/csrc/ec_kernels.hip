@@ -2,29 +2,21 @@
  * ec_kernels.hip -- launchers of the gfx950 kernels in ec_kernels_impl.h
  * (see that header for the kernels and the reference functions they replace).
  *
- * Shipped configuration (tools/kbench A/B runs, profiles/kbench_r01.log):
- *   encode   compile-time Vandermonde rows for 2+1, 4+2, 8+4, 16+4;
- *            W = 4 / 2 / 1 / 1 dwords per plane per lane (VGPR budget)
- *   stores   non-temporal for every combine and for the k > 4 encoders;
- *            default for the 2+1 / 4+2 encoders, where they cost 3-4 %
- *            (profiles/kbench_r01_nts.log).  Without them the output lines
- *            sit dirty in the per-XCD L2 and are written back at the kernel
- *            boundary: 8+4 decode of a 64K-stripe batch (BASELINE
- *            configs[2]) 0.58 -> 0.70 of 8 TB/s, 8+4 encode 0.655 -> 0.670
- *   combine  one tile per block, staged by LDS-DMA (global_load_lds_dwordx4)
- *            into a plane-major tile; outputs stored straight from registers.
- *            8-stripe tiles; 8 / 4 / 16 waves per block for k <= 4 / 8 / 16
- *            (8 waves for 8+4 mixed patterns, 16 for full 8+4 decodes of
- *            up to 128K stripes).  At k = 16 two 16-wave
- *            blocks fill all 32 wave slots of a CU, which hides the
- *            compare-tree dispatch of the multiply.  Two back-to-back
- *            processes, 21 interleaved rounds (profiles/kbench_r01_nw*.log):
- *            4+2 0x3C 0.707 -> 0.725-0.736, 8+4 dense 0.665 -> 0.669-0.676,
- *            8+4 mixed 0.651-0.673, 16+4 0.43 -> 0.506 of 8 TB/s.
- *            History: LDS-DMA over register staging took 8+4 decode
- *            0.57 -> 0.66 and 16+4 0.24 -> 0.42; the plane-major tile (one
- *            LDS address per input instead of five) 16+4 0.43 -> 0.45
- *            (profiles/kbench_r01_combine_pm.log)
+ * Shipped configuration (r03; one-process A/Bs in tools/kbench/kb3.hip,
+ * profiles/kb3_r03*.log, and round 1-2's tools/kbench/kbench.hip):
+ *   encode   4+2, 8+4: narrow-tile encoders (ec_encode_tile_t, 4-stripe
+ *            tiles, per-wave 2 KiB row runs); 16+4: the 8-stripe tile
+ *            encoder; 2+1, misaligned inputs and pinned-host (zero-copy)
+ *            calls: the register-resident ec_encode_vander
+ *   combine  k <= 8 (decode, heal, mixed, sorted slots, device pattern
+ *            table): the narrow-tile ec_combine_n, 4 or 8 waves; k > 8: the
+ *            8-stripe ec_combine, 16 waves (two blocks fill a CU's 32 wave
+ *            slots); both stage by LDS-DMA into a plane-major tile and
+ *            multiply by a jump into the searched XOR programs
+ *   stores   non-temporal on every device-path kernel except the 2+1 / 4+2
+ *            register encoders (profiles/kbench_r01_nts.log)
+ *   host     pinned buffers: the zero-copy kernels (ec_combine_zc,
+ *            ec_encode_vander_zc), 1 KiB requests over PCIe
  */
 #include <hip/hip_runtime.h>
 
@@ -90,36 +82,33 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-/* NW: waves per block for a single pattern; NWM: for mixed patterns;
- * JTS / JTM: the multiply dispatch for single / mixed patterns (ec_combine's
- * JT: 0 the compiler's switch, 1 the jump table of ec_gf8_asm.h, 3 the
- * whole-row asm block of ec_gf8_row.h) */
-template <int K, int TS, int NW, int NWM, bool NTS, int JTS, int JTM, bool SL = false,
-          int OT = 0>
+/* The 8-stripe ec_combine (k > 8): single pattern, mixed patterns (kernel
+ * arguments or, PG, the device table), or sorted slots (SL). */
+template <int K, int NW, bool NTS, bool SL = false>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     /* sorted slots: every pattern's run may carry up to 7 padding slots */
-    const uint64_t g = SL ? (a.nstripes + 8ull * a.npatterns) / 8 + 1 : combine_grid<TS>(a.nstripes);
+    const uint64_t g = SL ? (a.nstripes + 8ull * a.npatterns) / 8 + 1 : combine_grid<1>(a.nstripes);
     if (g == 0)
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    const size_t lds = combine_lds<TS>(a.k) + (OT && OT != 4 ? combine_lds<TS>(a.rows) : 0);
+    const size_t lds = combine_lds<1>(a.k);
     if (a.patg) {
         /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
-        const void *kern = (const void *)ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM, SL>;
+        const void *kern = (const void *)ec_combine<K, 1, NW, true, NTS, 2, true, true, 1, SL>;
         if (lds + kPatLdsBytes > (64u << 10) &&
-            ensure_lds_limit(kern, (int)(combine_lds<TS>(K) + kPatLdsBytes)) != 0)
+            ensure_lds_limit(kern, (int)(combine_lds<1>(K) + kPatLdsBytes)) != 0)
             return -EIO;
-        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, true, true, JTM, SL>),
-                           dim3((u32)g), dim3(NWM * 64), lds + kPatLdsBytes, s, a);
+        hipLaunchKernelGGL((ec_combine<K, 1, NW, true, NTS, 2, true, true, 1, SL>), dim3((u32)g),
+                           dim3(NW * 64), lds + kPatLdsBytes, s, a);
+    } else if (a.group_pattern) {
+        hipLaunchKernelGGL((ec_combine<K, 1, NW, true, NTS, 2, false, true, 1, SL>), dim3((u32)g),
+                           dim3(NW * 64), lds, s, a);
+    } else {
+        hipLaunchKernelGGL((ec_combine<K, 1, NW, false, NTS, 2, false, true, 1>), dim3((u32)g),
+                           dim3(NW * 64), lds, s, a);
     }
-    else if (a.group_pattern)
-        hipLaunchKernelGGL((ec_combine<K, TS, NWM, true, NTS, 2, false, true, JTM, SL, 1, SL ? 0 : OT>),
-                           dim3((u32)g), dim3(NWM * 64), lds, s, a);
-    else
-        hipLaunchKernelGGL((ec_combine<K, TS, NW, false, NTS, 2, false, true, JTS, false, 1, OT>),
-                           dim3((u32)g), dim3(NW * 64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -162,53 +151,15 @@ int launch_encode_tile(hipStream_t s, uint64_t nstripes, const void *in, void *c
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-int output_tile_mode(const CombineArgs &a);
-
-/* 4+2: the encode matrix (row i: (i+1)^(3-j), ec-method.c:22-36) as one
- * ec_combine pattern over the stripe-major input */
-int launch_encode_42_combine(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
-{
-    static ecd_combine_desc_t d; /* pattern part built once; pointers per call */
-    static std::once_flag once;
-    std::call_once(once, [] {
-        memset(&d, 0, sizeof(d));
-        d.k = 4;
-        d.rows = 6;
-        d.in_stride = 4 * ECD_CHUNK;
-        d.out_stride = ECD_CHUNK;
-        d.npatterns = 1;
-        d.pat_bytes = 4 + 6 * 4;
-        for (u32 p = 0; p < 4; ++p)
-            d.pat[p] = (uint8_t)p;
-        for (u32 r = 0; r < 6; ++r)
-            for (u32 j = 0; j < 4; ++j)
-                d.pat[4 + r * 4 + j] = (uint8_t)gf_pow_c(r + 1, 3 - (int)j);
-    });
-    ecd_combine_desc_t c;
-    memcpy(&c, &d, offsetof(ecd_combine_desc_t, pat) + 4 + 6 * 4);
-    c.nstripes = nstripes;
-    for (u32 p = 0; p < 4; ++p)
-        c.in_base[p] = static_cast<const uint8_t *>(in) + p * ECD_CHUNK;
-    for (u32 r = 0; r < 6; ++r)
-        c.out_base[r] = out[r];
-    CombineArgs a;
-    const int rc = ecdk_pack_args(&c, &a);
-    if (rc)
-        return rc;
-    return output_tile_mode(a) == 2 ? launch_combine<4, 1, 16, 16, true, 1, 1, false, 2>(s, a)
-                                    : launch_combine<4, 1, 16, 16, true, 1, 1>(s, a);
-}
-
 } // namespace
 
-/* EC_MI355X_ENC=0 keeps the register-resident encoder for every geometry,
- * =1 the round-2 choice (8-stripe tile encoders), =2 those at every size
- * (A/B runs only); unset = the narrow-tile encoders (3). */
-static int enc_mode()
+/* EC_MI355X_ENC=0 keeps the register-resident encoder for every geometry
+ * (A/B runs); unset = the tile encoders. */
+static bool enc_tiles()
 {
-    static const int v = [] {
+    static const bool v = [] {
         const char *e = getenv("EC_MI355X_ENC");
-        return e && (*e == '0' || *e == '1' || *e == '2') ? *e - '0' : 3;
+        return !(e && *e == '0');
     }();
     return v;
 }
@@ -244,25 +195,20 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
      * input at any other alignment (a tensor slice) keeps the
      * register-resident encoder, whose loads take any byte address */
     const bool aligned = !((uintptr_t)in & 15);
-    /* narrow-tile encoders, same A/B (ms per GiB unless noted): 4+2 0.438 ->
-     * 0.423 (6 waves, direct products), 8+4 0.443 -> 0.411 and 64K-stripe
-     * batches 0.126 -> 0.095 ms (12 waves, Horner: one row per wave, and the
-     * 2 KiB row runs remove the 64-B segment writes of the register
-     * encoder, PMC 1.10x); 16+4 keeps the 8-stripe tile encoder (0.432
-     * against 0.453) */
-    if (!zc && aligned && enc_mode() == 3) {
+    /* narrow-tile encoders, kb3 A/B against round 2's encoders (ms per GiB
+     * unless noted, profiles/kb3_r03d.log): 4+2 0.438 -> 0.423 (6 waves,
+     * direct products), 8+4 0.443 -> 0.411 and 64K-stripe batches 0.126 ->
+     * 0.095 ms (12 waves, Horner: one row per wave; the 2 KiB row runs also
+     * remove the 64-B segment writes of the register encoder, PMC 1.10x);
+     * 16+4 keeps the 8-stripe tile encoder (0.432 against 0.453) */
+    if (!zc && aligned && enc_tiles()) {
         if (k == 4 && n == 6)
             return launch_encode_narrow<4, 6, 6, true>(s, nstripes, in, out);
         if (k == 8 && n == 12)
             return launch_encode_narrow<8, 12, 12, false>(s, nstripes, in, out);
+        if (k == 16 && n == 20)
+            return launch_encode_tile<16, 20, 16, false, 1>(s, nstripes, in, out);
     }
-    const bool tiles = !zc && enc_mode() != 0 && aligned;
-    if (tiles && k == 4 && n == 6)
-        return launch_encode_42_combine(s, nstripes, in, out);
-    if (tiles && k == 8 && n == 12 && (nstripes > (1u << 17) || enc_mode() == 2))
-        return launch_encode_tile<8, 12, 16, true, 2>(s, nstripes, in, out);
-    if (tiles && k == 16 && n == 20)
-        return launch_encode_tile<16, 20, 16, false, 1>(s, nstripes, in, out);
     if (k == 2 && n == 3)
         return launch_vander<2, 3, 4>(s, nstripes, in, out, zc);
     if (k == 4 && n == 6)
@@ -556,59 +502,6 @@ int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32
     return enqueue_upload(s, w, *tab);
 }
 
-/* EC_MI355X_NW4 / _NW8 / _NW16 = 4, 8 or 16: waves per block of every
- * k <= 4 / 4 < k <= 8 / k > 8 combine, single and mixed patterns alike
- * (tuning A/Bs only); unset = the shipped choice. */
-int nw_env(const char *name)
-{
-    const char *e = getenv(name);
-    const int n = e ? atoi(e) : 0;
-    return n == 4 || n == 8 || n == 16 ? n : 0;
-}
-
-int nw8_override()
-{
-    static const int v = nw_env("EC_MI355X_NW8");
-    return v;
-}
-
-int nw4_override()
-{
-    static const int v = nw_env("EC_MI355X_NW4");
-    return v;
-}
-
-int nw16_override()
-{
-    static const int v = nw_env("EC_MI355X_NW16");
-    return v;
-}
-
-/* Pattern groups of 1, 2 or 4 stripes: sort the stripes by pattern into
- * 8-slot tiles (ec_slots_*, ec_kernels_impl.h) and run the tile kernel over
- * the slot list.  Workspace: stream-ordered, freed after the launch. */
-template <bool NTS, typename F>
-int sorted_slots(hipStream_t s, const CombineArgs &a0, F tiles);
-
-template <bool NTS>
-int launch_combine_slots(hipStream_t s, const CombineArgs &a0)
-{
-    return sorted_slots<NTS>(s, a0, [](hipStream_t st, const CombineArgs &a) {
-        /* waves per block: 4 for k <= 4 (1-/4-stripe groups of 4+2 0.49 ->
-         * 0.45 ms per GiB against 8), 8 for k <= 8 (4 and 16 slower), same
-         * box through this launcher (profiles/ab_slots_r02z.log) */
-        if (a.k <= 4)
-            return nw4_override() == 16  ? launch_combine<4, 1, 16, 16, NTS, 1, 1, true>(st, a)
-                   : nw4_override() == 8 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, true>(st, a)
-                                         : launch_combine<4, 1, 4, 4, NTS, 1, 1, true>(st, a);
-        if (a.k <= 8)
-            return nw8_override() == 16  ? launch_combine<8, 1, 16, 16, NTS, 1, 1, true>(st, a)
-                   : nw8_override() == 4 ? launch_combine<8, 1, 4, 4, NTS, 1, 1, true>(st, a)
-                                         : launch_combine<8, 1, 8, 8, NTS, 1, 1, true>(st, a);
-        return launch_combine<16, 1, 16, 16, NTS, 1, 1, true>(st, a);
-    });
-}
-
 /* Pattern groups below one tile: sort the stripes by pattern into slot
  * runs padded to 8 (ec_slots_*), then tiles(stream, args-with-slots). */
 template <bool NTS, typename F>
@@ -647,76 +540,7 @@ int sorted_slots(hipStream_t s, const CombineArgs &a0, F tiles)
     return rc;
 }
 
-/* EC_MI355X_JT=0 / 1 forces the switch / the jump table for every k
- * (tuning A/Bs on one box, tools/ab_jt.sh); unset = the shipped choice.
- * (3, the whole-row asm block of ec_gf8_row.h, was A/B'd the same way in
- * r02z and is not built into the library: profiles/ab_row_r02z.log.) */
-int jt_override()
-{
-    static const int v = [] {
-        const char *e = getenv("EC_MI355X_JT");
-        return e && (*e == '0' || *e == '1' || *e == '4') ? *e - '0' : -1;
-    }();
-    return v;
-}
-
-/* Output tile (ec_combine OT) for k <= 4: the rows of a stripe are one
- * contiguous run of the output (a full decode into stripe-major data) and
- * the patterns are in the argument segment.  Same box through this
- * launcher, EC_MI355X_OT alternating, 40 launches after 20
- * (profiles/ab_ot_r02z.log): 4+2 decode 0.358-0.384 -> 0.346-0.359 ms per
- * GiB (8 more rounds of 20 launches after 5, profiles/ab_ot42_r02z.log:
- * median 0.366 -> 0.347), 4+2 mixed 0.361-0.364 -> 0.353-0.358; for k = 8
- * it loses (1 GiB
- * decode 0.367-0.379 -> 0.381, 64K-stripe batches 0.092-0.097 -> 0.099),
- * so k = 8 keeps the register stores.  EC_MI355X_OT=0 turns it off (A/B). */
-/* 0: no output tile; 1: stripe-major run (full decode); 2: fragment rows
- * (out_stride = 512, EC_MI355X_OT=2 only: A/B); EC_MI355X_OT=3: stripe-major
- * runs for k <= 8 too (A/B) */
-int output_tile_mode(const CombineArgs &a)
-{
-    static const int mode0 = [] {
-        const char *e = getenv("EC_MI355X_OT");
-        return e && (*e == '0' || *e == '2' || *e == '3' || *e == '4') ? *e - '0' : 1;
-    }();
-    int mode = mode0;
-    if (mode == 4 && a.k > 8 && !a.patg && !a.group_pattern && a.rows <= a.k &&
-        a.out_stride == (uint64_t)a.rows * ECD_CHUNK && !((uintptr_t)a.out_base[0] & 15)) {
-        for (u32 r = 1; r < a.rows; ++r)
-            if (a.out_base[r] != a.out_base[0] + (size_t)r * ECD_CHUNK)
-                return 0;
-        return 4;                 /* k = 16 in-place output tile (A/B) */
-    }
-    if (mode == 4)
-        mode = 1;
-    if (mode == 0 || a.k > (mode == 3 ? 8u : 4u) || a.patg ||
-        (a.group_pattern && a.group_shift < 3))
-        return 0;
-    for (u32 r = 0; r < a.rows; ++r)
-        if ((uintptr_t)a.out_base[r] & 15)
-            return 0;
-    if (mode == 2 && a.out_stride == ECD_CHUNK)
-        return 2;
-    if (a.out_stride != (uint64_t)a.rows * ECD_CHUNK)
-        return 0;
-    for (u32 r = 1; r < a.rows; ++r)
-        if (a.out_base[r] != a.out_base[0] + (size_t)r * ECD_CHUNK)
-            return 0;
-    return 1;
-}
-
 /* ------------------------------------------------ narrow tiles (r03) */
-
-/* EC_MI355X_NARROW=0 restores the 8-stripe ec_combine for every device
- * combination (A/B runs); unset = the narrow-tile kernels. */
-bool narrow_on()
-{
-    static const bool v = [] {
-        const char *e = getenv("EC_MI355X_NARROW");
-        return !(e && *e == '0');
-    }();
-    return v;
-}
 
 template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG, bool SL>
 int launch_n1(hipStream_t s, const CombineArgs &a, uint64_t g)
@@ -748,9 +572,6 @@ int launch_narrow_k(hipStream_t s, const CombineArgs &a)
     });
 }
 
-template <bool NTS>
-int launch_combine_r02(hipStream_t s, const CombineArgs &a);
-
 /* The device combine for k <= 8: narrow tiles with per-wave output staging
  * (tools/kbench/kb3.hip, one process, 7 interleaved rounds against the
  * round-2 dispatch, profiles/kb3_r03d.log, ms per GiB unless noted):
@@ -759,97 +580,23 @@ int launch_combine_r02(hipStream_t s, const CombineArgs &a);
  *   8+4 decode, 64K stripes 0.096 -> 0.083   8 waves (small batches)
  *   8+4 heal (4 rows)       0.316 -> 0.263   4 waves
  *   8+4 mixed, 16 masks     0.395 -> 0.375   4 waves
- * k = 16 keeps the 8-stripe ec_combine: 16+4 decode 0.406 against 0.421 at
- * best narrow (8 waves, register stores), mixed 0.395 against 0.442. */
-template <bool NTS>
-int launch_narrow(hipStream_t s, const CombineArgs &a)
-{
-    if (a.k <= 4)
-        return launch_narrow_k<4, 4, 1, NTS>(s, a);
-    if (a.nstripes <= (1u << 17))
-        return launch_narrow_k<8, 8, 1, NTS>(s, a);
-    return launch_narrow_k<8, 4, 1, NTS>(s, a);
-}
-
+ * k = 16 keeps the 8-stripe ec_combine with 16 waves: 16+4 decode 0.406
+ * against 0.421 at best narrow (8 waves, register stores), mixed 0.395
+ * against 0.442.  Groups below a tile (8 stripes for ec_combine, 4 for the
+ * narrow tiles) are sorted into slots first. */
 template <bool NTS>
 int launch_combine_k(hipStream_t s, const CombineArgs &a)
 {
-    return narrow_on() && a.k <= 8 ? launch_narrow<NTS>(s, a) : launch_combine_r02<NTS>(s, a);
-}
-
-/* Round 2's 8-stripe ec_combine dispatch (EC_MI355X_NARROW=0, A/B). */
-template <bool NTS>
-int launch_combine_r02(hipStream_t s, const CombineArgs &a)
-{
-    const int jt = jt_override();
-    if (a.k <= 4 && jt != 0 && !(a.group_pattern && a.group_shift < 3)) {
-        switch (nw4_override()) {
-        case 4: return launch_combine<4, 1, 4, 4, NTS, 1, 1>(s, a);
-        case 8: return launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
-        case 16: return launch_combine<4, 1, 16, 16, NTS, 1, 1>(s, a);
-        default: break;
-        }
-    }
-    if (a.k > 4 && a.k <= 8 && jt != 0 && !(a.group_pattern && a.group_shift < 3)) {
-        switch (nw8_override()) {
-        case 4: return launch_combine<8, 1, 4, 4, NTS, 1, 1>(s, a);
-        case 8: return launch_combine<8, 1, 8, 8, NTS, 1, 1>(s, a);
-        case 16: return launch_combine<8, 1, 16, 16, NTS, 1, 1>(s, a);
-        default: break;
-        }
-    }
-    if (a.k > 8 && jt != 0 && !(a.group_pattern && a.group_shift < 3)) {
-        switch (nw16_override()) {
-        case 4: return launch_combine<16, 1, 4, 4, NTS, 1, 1>(s, a);
-        case 8: return launch_combine<16, 1, 8, 8, NTS, 1, 1>(s, a);
-        default: break;
-        }
-    }
-    if (a.group_pattern && a.group_shift < 3)
-        return launch_combine_slots<NTS>(s, a);
-    /* 8-stripe tiles (a tile never straddles two pattern groups: shift >= 3) */
-    /* The multiply dispatch is the jump table (ec_gf8_asm.h) for every k:
-     * same-box A/B through this launcher, EC_MI355X_JT=0/1 alternating
-     * (profiles/ab_jt_r02f.log): 8+4 decode 1 GiB 0.440 -> 0.392-0.403 ms,
-     * 16+4 mixed 64 masks 0.591-0.608 -> 0.505 ms, 4+2 0x3C 0.365 -> 0.360,
-     * 8+4 64K-stripe batches and 8+4 mixed ties.  EC_MI355X_JT=0 keeps the
-     * compiler's switch for A/Bs. */
-    const bool sw = jt == 0;
-    if (jt == 4 && a.k <= 8) {     /* software-pipelined loop (A/B) */
-        if (a.k <= 4)
-            return launch_combine<4, 1, 8, 8, NTS, 4, 4>(s, a);
-        if (a.rows > 4)
-            return launch_combine<8, 1, 16, 16, NTS, 4, 4>(s, a);
-        return launch_combine<8, 1, 4, 16, NTS, 4, 4>(s, a);
-    }
-    const int ot = sw ? 0 : output_tile_mode(a);
     if (a.k <= 4)
-        return sw        ? launch_combine<4, 1, 8, 8, NTS, 0, 0>(s, a)
-               : ot == 1 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, false, 1>(s, a)
-               : ot == 2 ? launch_combine<4, 1, 8, 8, NTS, 1, 1, false, 2>(s, a)
-                         : launch_combine<4, 1, 8, 8, NTS, 1, 1>(s, a);
-    if (a.k <= 8 && ot == 1 && a.rows > 4)         /* EC_MI355X_OT=3 (A/B) */
-        return launch_combine<8, 1, 16, 16, NTS, 1, 1, false, 1>(s, a);
-    if (a.k <= 8) {
-        /* Full decodes (rows > 4) use 16-wave blocks, single and mixed
-         * patterns.  r01 (switch dispatch): 64K-stripe batches 99.5 -> 91 us
-         * for 0xFF0 against 4 waves, 1 GiB 2 % slower (ab_r01_nw16.log).
-         * r02z (jump table), same box through this launcher, EC_MI355X_NW8
-         * alternating (profiles/ab_nw8_r02z.log): 1 GiB 0.381-0.385 ms at 4
-         * waves -> 0.369-0.381 at 16; mixed patterns in 1024-stripe groups
-         * (BASELINE configs[4]) 0.449-0.466 ms at 8 waves -> 0.388-0.393 at
-         * 16; 64K-stripe 0xEB5 batches 16 ~ shipped, 8 and 4 slower.
-         * Heal-shaped calls (rows <= 4) keep 4 waves (all sizes tie). */
-        if (a.rows > 4)
-            return sw ? launch_combine<8, 1, 16, 8, NTS, 0, 0>(s, a)
-                      : launch_combine<8, 1, 16, 16, NTS, 1, 1>(s, a);
-        return sw ? launch_combine<8, 1, 4, 8, NTS, 0, 0>(s, a)
-                  : launch_combine<8, 1, 4, 16, NTS, 1, 1>(s, a);
-    }
-    if (ot == 4)                                /* EC_MI355X_OT=4 (A/B) */
-        return launch_combine<16, 1, 16, 16, NTS, 1, 1, false, 4>(s, a);
-    return sw ? launch_combine<16, 1, 16, 16, NTS, 0, 0>(s, a)
-           : launch_combine<16, 1, 16, 16, NTS, 1, 1>(s, a);
+        return launch_narrow_k<4, 4, 1, NTS>(s, a);
+    if (a.k <= 8)
+        return a.nstripes <= (1u << 17) ? launch_narrow_k<8, 8, 1, NTS>(s, a)
+                                        : launch_narrow_k<8, 4, 1, NTS>(s, a);
+    if (a.group_pattern && a.group_shift < 3)
+        return sorted_slots<NTS>(s, a, [](hipStream_t st, const CombineArgs &b) {
+            return launch_combine<16, 16, NTS, true>(st, b);
+        });
+    return launch_combine<16, 16, NTS>(s, a);
 }
 
 /* pack, then launch; -E2BIG from the packer means "use a device table" */
@@ -985,14 +732,9 @@ int combine_realigned(hipStream_t s, const ecd_combine_desc_t *d)
 
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
 {
-    /* EC_MI355X_NTS=0: default-policy stores on the device path (A/B only) */
-    static const bool nts = [] {
-        const char *e = getenv("EC_MI355X_NTS");
-        return !(e && *e == '0');
-    }();
     if (inputs_misaligned(d))
-        return nts ? combine_realigned<true>(s, d) : combine_realigned<false>(s, d);
-    return nts ? combine_any<true>(s, d) : combine_any<false>(s, d);
+        return combine_realigned<true>(s, d);
+    return combine_any<true>(s, d);
 }
 
 /* Host-buffer path: every buffer is pinned host memory read / written over

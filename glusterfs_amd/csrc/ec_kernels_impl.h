@@ -756,27 +756,19 @@ __device__ __forceinline__ uint64_t slot_stripe(const CombineArgs &a, uint64_t s
  * one lane address serves all 8 planes of an input (ds_read2st64_b64 with
  * immediate plane offsets) -- the earlier chunk-major tile needed an
  * XOR-rotated plane slot, hence 5 address VALUs per input. */
-/* JT: 0 = the compiler's switch, 1 = the jump table of ec_gf8_asm.h, 2 = the
- * same with 32-byte-aligned bodies, 4 = a software-pipelined loop over the
- * <= 4-temporary programs of ec_gf8_asm_t4.h.  (r02z also A/B'd a whole-row asm block
- * and grouped waits on the staged inputs; neither was faster: DESIGN.md 3.4,
- * code in commit 87d127c.)
+/* JT: 0 = the compiler's switch, 1 = the jump table of ec_gf8_asm.h.
+ * (Retired, with their A/B logs in DESIGN.md 3.4: the whole-row asm block
+ * and grouped staging waits (r02z, commit 87d127c), the software-pipelined
+ * loop over <= 4-temporary programs (JT = 4) and the output tiles (OT) for
+ * fragment outputs and k >= 8 (r02, commit 1c377cb); the narrow kernels
+ * below took over every k <= 8 call in r03.)
  * SLOTS: mixed patterns with groups below a tile (1, 2, 4 stripes): the
  * stripes were sorted by pattern into 8-slot tiles (ec_slots_* kernels), and
  * the block reads its tile's stripes from the slot list. */
-/* OT: the output rows are assembled in LDS after the input tile and the
- * block writes them in destination order, 16 B per lane, 1 KiB per wave
- * instruction, instead of each wave storing 64-B plane segments at a
- * stride straight from its registers.  OT = 1: stripe-major outputs
- * (out_base[r] = out_base[0] + r * 512, out_stride = rows * 512: full
- * decodes), stripe s / row r at (s * rows + r) * 512, the tile one run;
- * OT = 2: fragment outputs (out_stride = 512: encode, heal), row r / stripe
- * s at (r * 8 + s) * 512, one run per row.  8-stripe tiles, not PG / SLOTS. */
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1, int OT = 0>
+          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
-    static_assert(!OT || (TS == 1 && CW == 2 && !PG && !SLOTS), "output tile: 8-stripe tiles");
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
     /* CW: dwords per plane per lane in the compute phase; a wave item covers
      * SPI = 4*CW stripes of one output row */
@@ -795,7 +787,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             return;             /* the grid is sized for the worst padding */
     }
     /* a sorted tile is one pattern's: take it from the tile's first stripe
-     * (never padding: runs are padded at their end) */
+     * (never padding: runs are padded at their end, to 8 slots) */
     const uint64_t tp = SLOTS ? slot_stripe<SLOTS>(a, t0, nslots) : t0;
     const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp), lane, lds + k * (T * ECD_CHUNK));
 
@@ -828,60 +820,6 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     /* compute: (row, 8-stripe subtile) items spread over the NW waves */
     const u32 cs = lane / LPS, cc = lane % LPS;
     const u32 items = a.rows * IPT;
-    if constexpr (OT == 4) {
-        /* OT = 4: the output tile of OT = 1 assembled in place of the input
-         * tile once every wave is done reading it (no extra LDS; needs one
-         * item per wave: rows <= NW, checked by the launcher) */
-        static_assert(JT == 1 && CW == 2 && TS == 1, "in-place output tile: jump table, CW 2");
-        u32 acc[8][2], y[8][2];
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-            acc[b][0] = acc[b][1] = 0;
-        const bool has = wave < items;
-        const u32 r = has ? wave : 0u;
-        if (has) {
-            const uint8_t *col = lds + cs * 64u + cc * 8u;
-            const u32 rw = a.kw * (1 + r);
-            const u32 w0 = pw.word(a, rw);
-            const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
-            const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
-            const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
-            uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
-            uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
-#pragma unroll 1
-            for (u32 p = 0; p < k; ++p) {
-                const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
-                cl = (cl >> 8) | (ch << 56);
-                ch >>= 8;
-                if (c == 0)                  /* ec-code-c.c:11666-11676 */
-                    continue;
-                const uint8_t *src = col + p * (T * ECD_CHUNK);
-#pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    load_plane<2>(src + (u32)b * (T * 64u), y[b]);
-                ecgf::mul_xor_jt<2>(c, acc, y);
-            }
-        }
-        __syncthreads();                     /* the input tile is free */
-        if (has) {
-            uint8_t *o = lds + (cs * a.rows + r) * ECD_CHUNK + cc * 8u;
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-                *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
-        }
-        __syncthreads();
-        const u32 nst = (u32)(a.nstripes - t0 < T ? a.nstripes - t0 : T);
-        const u32 pieces = nst * a.rows * (ECD_CHUNK / 16);
-        uint8_t *dst = a.out_base[0] + t0 * a.out_stride;
-        for (u32 i = tid; i < pieces; i += NW * 64) {
-            const v4u v = *reinterpret_cast<const v4u *>(lds + i * 16u);
-            if constexpr (NTS)
-                __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(dst + i * 16u));
-            else
-                *reinterpret_cast<v4u *>(dst + i * 16u) = v;
-        }
-        return;
-    }
     for (u32 it = wave; it < items; it += NW) {
         const u32 r = it / IPT, s = (it % IPT) * SPI + cs;
         const uint8_t *col = lds + s * 64u + cc * (4u * CW);
@@ -892,48 +830,6 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
         const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
         const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
         u32 acc[8][CW], y[8][CW];
-        if constexpr (JT == 4) {
-            /* software-pipelined: the next input's planes are read from LDS
-             * before the current multiply, so their latency overlaps the
-             * dispatch and the body; zero coefficients run table entry 0 */
-            static_assert(CW == 2, "pipelined loop: 2 dwords per lane");
-            u32 yn[8][2];
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                acc[b][0] = acc[b][1] = 0;
-                load_plane<2>(col + (u32)b * (T * 64u), y[b]);
-            }
-            uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
-            uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
-#pragma unroll 1
-            for (u32 p = 0; p < k; ++p) {
-                const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
-                cl = (cl >> 8) | (ch << 56);
-                ch >>= 8;
-                const uint8_t *nx = col + (p + 1 < k ? p + 1 : p) * (T * ECD_CHUNK);
-#pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    load_plane<2>(nx + (u32)b * (T * 64u), yn[b]);
-                ecgf::mul_xor_jt4(c, acc, y);
-#pragma unroll
-                for (int b = 0; b < 8; ++b) {
-                    y[b][0] = yn[b][0];
-                    y[b][1] = yn[b][1];
-                }
-            }
-            if constexpr (OT) {
-                uint8_t *o = lds + k * (T * ECD_CHUNK) + (OT == 1 ? s * a.rows + r : r * T + s) * ECD_CHUNK + cc * 8u;
-#pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
-            } else {
-                const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
-                if (ost != kNoSlot)
-                    store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW),
-                                         acc);
-            }
-            continue;
-        }
 #pragma unroll
         for (int b = 0; b < 8; ++b)
 #pragma unroll
@@ -957,45 +853,13 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
             for (int b = 0; b < 8; ++b)
                 load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
             if constexpr (JT && CW == 2)
-                ecgf::mul_xor_jt<CW, JT == 2>(c, acc, y);
+                ecgf::mul_xor_jt<CW>(c, acc, y);
             else
                 ecgf::mul_xor_rt<CW, CSE>(c, acc, y);
         }
-        if constexpr (OT) {
-            uint8_t *o = lds + k * (T * ECD_CHUNK) + (OT == 1 ? s * a.rows + r : r * T + s) * ECD_CHUNK + cc * 8u;
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-                *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
-        } else {
-            const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
-            if (ost != kNoSlot)
-                store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
-        }
-    }
-    if constexpr (OT) {
-        __syncthreads();
-        /* the tile's stripes are one contiguous run of the output */
-        const uint8_t *otile = lds + k * (T * ECD_CHUNK);
-        const u32 nst = (u32)(a.nstripes - t0 < T ? a.nstripes - t0 : T);
-        const u32 per_row = nst * (ECD_CHUNK / 16);     /* 16-B pieces of one row */
-        const u32 pieces = per_row * a.rows;
-        for (u32 i = tid; i < pieces; i += NW * 64) {
-            const uint8_t *src;
-            uint8_t *dst;
-            if constexpr (OT == 1) {
-                src = otile + i * 16u;
-                dst = a.out_base[0] + t0 * a.out_stride + i * 16u;
-            } else {
-                const u32 r = i / per_row, w = i % per_row;
-                src = otile + (r * T) * ECD_CHUNK + w * 16u;
-                dst = a.out_base[r] + t0 * ECD_CHUNK + w * 16u;
-            }
-            const v4u v = *reinterpret_cast<const v4u *>(src);
-            if constexpr (NTS)
-                __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(dst));
-            else
-                *reinterpret_cast<v4u *>(dst) = v;
-        }
+        const uint64_t ost = slot_stripe<SLOTS>(a, t0 + s, nslots);
+        if (ost != kNoSlot)
+            store_chunk<CW, NTS>(a.out_base[r] + ost * a.out_stride + cc * (4u * CW), acc);
     }
 }
 
@@ -1065,8 +929,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
 #pragma unroll
             for (int b = 0; b < 8; ++b)
                 y[b][0] = *reinterpret_cast<const u32 *>(src + (u32)b * (T * 64u));
-            u32 t[ECGF_ASM_TEMPS][1];
-            ECGF_ASM_DISPATCH_W1(acc, y, t, c);
+            ecgf::mul_xor_jt<1>(c, acc, y);
         }
         if constexpr (WOT) {
             store_chunks_via_lds<T, 1, NTS, WOT>(slice, acc, cs, cc, lane, [&](u32 s) {

@@ -116,17 +116,14 @@ static FragPtrs frag_ptrs(uint8_t *b, uint64_t nst, int n)
     return f;
 }
 
-/* round 2's device encode (ecdk_encode_vander with EC_MI355X_ENC=1) */
-static int encode_r02(hipStream_t st, int k, int n, uint64_t nst, const uint8_t *in,
-                      void *const *o)
+/* The round-2 baselines these kernels were first timed against (the 8-stripe
+ * encoders / ec_combine dispatch) left the library when the narrow kernels
+ * shipped; their numbers are in profiles/kb3_r03d.log.  "shipped" below is
+ * the library's current dispatch. */
+static int encode_shipped(hipStream_t st, int k, int n, uint64_t nst, const uint8_t *in,
+                          void *const *o)
 {
-    if (k == 4)
-        return launch_encode_42_combine(st, nst, in, o);
-    if (k == 8 && nst > (1u << 17))
-        return launch_encode_tile<8, 12, 16, true, 2>(st, nst, in, o);
-    if (k == 8)
-        return launch_vander<8, 12, 1, true>(st, nst, in, o, false);
-    return launch_encode_tile<16, 20, 16, false, 1>(st, nst, in, o);
+    return ecdk_encode_vander(st, k, n, nst, in, o, false);
 }
 
 static void add_shipped_encode(std::vector<Variant> &v, const char *nm, int k, int n,
@@ -136,7 +133,7 @@ static void add_shipped_encode(std::vector<Variant> &v, const char *nm, int k, i
                      void *o[ECD_MAX_ROWS];
                      for (int i = 0; i < n; ++i)
                          o[i] = f.p[i];
-                     if (encode_r02(st, k, n, nst, in, o))
+                     if (encode_shipped(st, k, n, nst, in, o))
                          exit(7);
                  }, f.p[n - 1], (size_t)nst * ECD_CHUNK});
 }
@@ -184,7 +181,7 @@ static void add_shipped_combine(std::vector<Variant> &v, const char *nm, const C
                                 double bytes, uint8_t *out, size_t ob)
 {
     v.push_back({nm, bytes, [=](hipStream_t st) {
-                     if (launch_combine_r02<true>(st, *a))
+                     if (launch_combine_k<true>(st, *a))
                          exit(8);
                  }, out, ob});
 }
@@ -224,7 +221,7 @@ int main(int argc, char **argv)
     if (want(groups, "enc16")) {
         const uint64_t nst = user / (16 * ECD_CHUNK);
         FragPtrs f = frag_ptrs(bufB, nst, 20);
-        add_shipped_encode(v, "r02 (tile T8 CW1 NW16)", 16, 20, nst, bufA, f);
+        add_shipped_encode(v, "shipped (tile T8 CW1 NW16)", 16, 20, nst, bufA, f);
         add_tile_t<16, 20, 4, 4, false, true>(v, "T4 NW4 WOT", nst, bufA, f);
         add_tile_t<16, 20, 4, 5, false, true>(v, "T4 NW5 WOT", nst, bufA, f);
         add_tile_t<16, 20, 4, 10, false, true>(v, "T4 NW10 WOT", nst, bufA, f);
@@ -237,7 +234,7 @@ int main(int argc, char **argv)
         for (int big = 0; big < 2; ++big) {
             const uint64_t nst = big ? user / (8 * ECD_CHUNK) : 65536;
             FragPtrs f = frag_ptrs(bufB, nst, 12);
-            add_shipped_encode(v, big ? "r02 (tile T8 CW2 NW16 direct)" : "r02 (vander W1)",
+            add_shipped_encode(v, "shipped (narrow T4 NW12)",
                                8, 12, nst, bufA, f);
             add_tile_t<8, 12, 8, 12, true, true>(v, "T8 NW12 direct WOT", nst, bufA, f);
             add_tile_t<8, 12, 4, 4, true, true>(v, "T4 NW4 direct WOT", nst, bufA, f);
@@ -253,7 +250,7 @@ int main(int argc, char **argv)
     if (want(groups, "enc4")) {
         const uint64_t nst = user / (4 * ECD_CHUNK);
         FragPtrs f = frag_ptrs(bufB, nst, 6);
-        add_shipped_encode(v, "r02 (combine NW16 jt)", 4, 6, nst, bufA, f);
+        add_shipped_encode(v, "shipped (narrow T4 NW6 direct)", 4, 6, nst, bufA, f);
         add_tile_t<4, 6, 8, 6, true, true>(v, "T8 NW6 direct WOT", nst, bufA, f);
         add_tile_t<4, 6, 4, 6, true, true>(v, "T4 NW6 direct WOT", nst, bufA, f);
         add_tile_t<4, 6, 4, 6, false, true>(v, "T4 NW6 WOT", nst, bufA, f);
@@ -275,7 +272,7 @@ int main(int argc, char **argv)
         const CombineArgs *a = make_args(K, rows, nst, fr, bufB, !heal, c);
         const double bytes = (double)nst * (K + rows) * ECD_CHUNK;
         const size_t ob = (size_t)nst * rows * ECD_CHUNK;
-        add_shipped_combine(v, "r02", a, bytes, bufB, ob);
+        add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
         add_combine_n<K, 8, 0>(v, "narrow NW8", a, bytes, bufB, ob);
         add_combine_n<K, 8, 1>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
         add_combine_n<K, 8, 2>(v, "narrow NW8 WOT/2", a, bytes, bufB, ob);
@@ -306,7 +303,7 @@ int main(int argc, char **argv)
         const CombineArgs *a = make_args(K, K, nst, fr, bufB, true, c);
         const double bytes = 2.0 * nst * K * ECD_CHUNK;
         const size_t ob = (size_t)nst * K * ECD_CHUNK;
-        add_shipped_combine(v, "r02", a, bytes, bufB, ob);
+        add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
         add_combine_n<K, 4, 0>(v, "narrow NW4", a, bytes, bufB, ob);
         add_combine_n<K, 4, 1>(v, "narrow NW4 WOT", a, bytes, bufB, ob);
         add_combine_n<K, 8, 1>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
@@ -364,7 +361,7 @@ int main(int argc, char **argv)
         }
         const double bytes = 2.0 * nst * K * ECD_CHUNK;
         const size_t ob = (size_t)nst * K * ECD_CHUNK;
-        add_shipped_combine(v, "r02", a, bytes, bufB, ob);
+        add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
         auto addm = [&](const char *nm, auto kern, int nw, size_t lds) {
             lds_attr((const void *)kern, lds);
             const uint64_t g = (nst + 3) / 4;

@@ -10,6 +10,7 @@
  *   tools/kbench/kbench [GiB=1] [rounds=7]
  */
 #include "../../glusterfs_amd/csrc/ec_kernels.hip"
+#include "ec_gf8_asm_t4.h"   /* the <= 4-temporary programs (kb_combine_pf) */
 
 #include <algorithm>
 #include <cstdio>
