@@ -566,8 +566,9 @@ def test_decode_mixed_short_runs(ec, oracle, k, n, group):
     padding (round 3: they looked their pattern up at slot ~0 and faulted).
     Every mask appears 1-3 times; checked group by group against the
     oracle's inverse."""
+    import math
     import torch
-    nmasks = 15
+    nmasks = min(15, math.comb(n, k))
     pool = _distinct_masks(n, k, nmasks, seed=group * 7 + k)
     ids = []
     rng = np.random.default_rng(k + group)
