@@ -877,7 +877,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": "ec_combine<K=4,TS=1,NW=8,NTS,JT,OT=1> (decode, jump-table multiply, output tile)",
+            "kernel": "ec_combine_n<K=4,NW=4,MIXED=0,NTS,WOT=1> (decode: 4-stripe tiles, "
+                      "jump-table multiply, per-wave 512-B output runs)",
             "algorithmic_bytes_per_launch": 2 * r["user"],
             "avg_launch_ms": round(kt * 1e3, 4),
         },

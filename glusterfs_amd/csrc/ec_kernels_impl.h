@@ -871,13 +871,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
  * the row's 4 chunks leave through the wave's LDS slice in 512-B runs (WOT
  * = 2: a half slice, two passes).  PG and SLOTS as in ec_combine (device
  * pattern table; sorted slots, whose runs are padded to 8 and so to 4). */
-/* PIPE: the p-loop unrolled by two with two input buffers, input p + 1's
- * LDS reads issued before input p's multiply (no register copies: the two
- * multiply sites are two copies of the one-dword bodies, together the size
- * of the two-dword table, ~53 KiB); zero coefficients run table entry 0, a
- * no-op. */
-template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG = false, bool SLOTS = false,
-          bool PIPE = false>
+template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG = false, bool SLOTS = false>
 __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
 {
     constexpr u32 T = 4;
@@ -936,33 +930,16 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
             for (int b = 0; b < 8; ++b)
                 d[b][0] = *reinterpret_cast<const u32 *>(src + (u32)b * (T * 64u));
         };
-        if constexpr (PIPE) {
-            u32 y1[8][1];
-            load_in(0, y);
+        /* (r03 also timed a software-pipelined form: the loop unrolled by
+         * two over two input buffers, input p + 1's reads issued before
+         * input p's multiply; it tied or lost at every k, kb3_r03g.log) */
 #pragma unroll 1
-            for (u32 p = 0; p < k; p += 2) {
-                const u32 c0 = next_c();
-                const u32 c1 = p + 1 < k ? next_c() : 0u;
-                if (p + 1 < k)
-                    load_in(p + 1, y1);
-                __builtin_amdgcn_sched_barrier(0);
-                ecgf::mul_xor_jt<1>(c0, acc, y);
-                __builtin_amdgcn_sched_barrier(0);
-                if (p + 2 < k)
-                    load_in(p + 2, y);
-                __builtin_amdgcn_sched_barrier(0);
-                ecgf::mul_xor_jt<1>(c1, acc, y1);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-#pragma unroll 1
-            for (u32 p = 0; p < k; ++p) {
-                const u32 c = next_c();
-                if (c == 0)                  /* ec-code-c.c:11666-11676 */
-                    continue;
-                load_in(p, y);
-                ecgf::mul_xor_jt<1>(c, acc, y);
-            }
+        for (u32 p = 0; p < k; ++p) {
+            const u32 c = next_c();
+            if (c == 0)                  /* ec-code-c.c:11666-11676 */
+                continue;
+            load_in(p, y);
+            ecgf::mul_xor_jt<1>(c, acc, y);
         }
         if constexpr (WOT) {
             store_chunks_via_lds<T, 1, NTS, WOT>(slice, acc, cs, cc, lane, [&](u32 s) {

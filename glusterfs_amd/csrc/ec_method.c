@@ -370,7 +370,8 @@ enum { ECM_OBS_CPU = 0, ECM_OBS_GPU_MAPPED = 1, ECM_OBS_GPU_PAGEABLE = 2 };
 static struct {
     uint64_t kbps;   /* user KB per second, EWMA; 0: no sample yet */
     uint32_t lost;   /* calls routed away from this engine since its last sample */
-    uint32_t pad[13];
+    uint32_t n;      /* samples taken (the first, a cold start, is dropped) */
+    uint32_t pad[12];
 } __attribute__((aligned(64))) ecm_obs[3][2][3];
 
 static int
@@ -396,12 +397,16 @@ obs_record(int eng, int op, uint32_t k, uint64_t user, uint64_t ns)
 
     if (user < ECM_OBS_MIN || ns == 0 || !ecm_x.adapt)
         return;
+    __atomic_store_n(&ecm_obs[eng][op][kbucket(k)].lost, 0, __ATOMIC_RELAXED);
+    /* the first call of an engine pays its cold start (page faults on fresh
+     * outputs, lazy set-up): a sample of it would bar the engine for long */
+    if (__atomic_fetch_add(&ecm_obs[eng][op][kbucket(k)].n, 1, __ATOMIC_RELAXED) == 0)
+        return;
     sample = user * 1000000ull / ns;                   /* KB/s = B/ns * 1e6 / 1e3 */
     old = __atomic_load_n(slot, __ATOMIC_RELAXED);
     do
-        upd = old ? old + ((int64_t)sample - (int64_t)old) / 8 : sample;
+        upd = old ? old + ((int64_t)sample - (int64_t)old) / 4 : sample;
     while (!__atomic_compare_exchange_n(slot, &old, upd, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED));
-    __atomic_store_n(&ecm_obs[eng][op][kbucket(k)].lost, 0, __ATOMIC_RELAXED);
 }
 
 static double
@@ -410,15 +415,19 @@ obs_gbps(int eng, int op, uint32_t k)
     return (double)__atomic_load_n(&ecm_obs[eng][op][kbucket(k)].kbps, __ATOMIC_RELAXED) / 1e6;
 }
 
-/* 1: send this call to the engine the router did not pick, to re-sample it */
+/* 1: send this call to the engine the router did not pick, to re-sample it
+ * (every 8th such call while the engine has fewer than 4 samples, then
+ * every 64th) */
 static int
 obs_explore(int eng, int op, uint32_t k, uint64_t user)
 {
     uint32_t *lost = &ecm_obs[eng][op][kbucket(k)].lost;
+    const uint32_t every =
+        __atomic_load_n(&ecm_obs[eng][op][kbucket(k)].n, __ATOMIC_RELAXED) < 4 ? 8 : 64;
 
     if (!ecm_x.adapt || user < ECM_OBS_EXPLORE)
         return 0;
-    return __atomic_add_fetch(lost, 1, __ATOMIC_RELAXED) % 64 == 0;
+    return __atomic_add_fetch(lost, 1, __ATOMIC_RELAXED) % every == 0;
 }
 
 static int
@@ -450,8 +459,8 @@ route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int mappe
     obs = user >= ECM_OBS_MIN
               ? obs_gbps(mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, op, ctx->k)
               : 0;
-    if (obs > 0)            /* the observed rate includes the call's latency */
-        gpu_us = (q + user) / (obs * 1e3);
+    if (obs > 0)            /* the observed rate includes the call's latency; a */
+        gpu_us = 1.1 * (q + user) / (obs * 1e3); /* near tie stays on the caller's CPU */
     else
         gpu_us = mapped ? (double)ecm_x.pin_us + (q + user) / ((double)ecm_x.pin_gbps * 1e3)
                         : (double)ecm_x.page_us +

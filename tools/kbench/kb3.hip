@@ -186,11 +186,11 @@ static void add_shipped_combine(std::vector<Variant> &v, const char *nm, const C
                  }, out, ob});
 }
 
-template <int K, int NW, int WOT, bool PIPE = false>
+template <int K, int NW, int WOT>
 static void add_combine_n(std::vector<Variant> &v, const char *nm, const CombineArgs *a,
                           double bytes, uint8_t *out, size_t ob)
 {
-    auto kern = ec_combine_n<K, NW, false, true, WOT, false, false, PIPE>;
+    auto kern = ec_combine_n<K, NW, false, true, WOT>;
     const size_t lds = combine_n_lds<NW, WOT>(K);
     lds_attr((const void *)kern, lds);
     const uint64_t g = (a->nstripes + 3) / 4;
@@ -274,13 +274,8 @@ int main(int argc, char **argv)
         const size_t ob = (size_t)nst * rows * ECD_CHUNK;
         add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
         add_combine_n<K, 8, 0>(v, "narrow NW8", a, bytes, bufB, ob);
-        add_combine_n<K, 8, 0, true>(v, "narrow NW8 pipe", a, bytes, bufB, ob);
         add_combine_n<K, 8, 1>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
-        add_combine_n<K, 8, 1, true>(v, "narrow NW8 WOT pipe", a, bytes, bufB, ob);
-        add_combine_n<K, 8, 2, true>(v, "narrow NW8 WOT/2 pipe", a, bytes, bufB, ob);
         add_combine_n<K, 4, 1>(v, "narrow NW4 WOT", a, bytes, bufB, ob);
-        add_combine_n<K, 4, 1, true>(v, "narrow NW4 WOT pipe", a, bytes, bufB, ob);
-        add_combine_n<K, 4, 0, true>(v, "narrow NW4 pipe", a, bytes, bufB, ob);
         run_group(title, v, rounds, iters, s);
         v.clear();
     };
@@ -306,8 +301,6 @@ int main(int argc, char **argv)
         const size_t ob = (size_t)nst * K * ECD_CHUNK;
         add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
         add_combine_n<K, 8, 1>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
-        add_combine_n<K, 8, 1, true>(v, "narrow NW8 WOT pipe", a, bytes, bufB, ob);
-        add_combine_n<K, 4, 1, true>(v, "narrow NW4 WOT pipe", a, bytes, bufB, ob);
         run_group("decode 8+4, 64K stripes", v, rounds, iters, s);
         v.clear();
     }
@@ -371,11 +364,7 @@ int main(int argc, char **argv)
                          }, bufB, ob});
         };
         addm("narrow NW4 WOT", ec_combine_n<K, 4, true, true, 1>, 4, combine_n_lds<4, 1>(K));
-        addm("narrow NW4 WOT pipe", ec_combine_n<K, 4, true, true, 1, false, false, true>, 4,
-             combine_n_lds<4, 1>(K));
         addm("narrow NW8", ec_combine_n<K, 8, true, true, 0>, 8, combine_n_lds<8, 0>(K));
-        addm("narrow NW8 pipe", ec_combine_n<K, 8, true, true, 0, false, false, true>, 8,
-             combine_n_lds<8, 0>(K));
         run_group(title, v, rounds, iters, s);
         v.clear();
     };
