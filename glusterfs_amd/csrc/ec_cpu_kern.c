@@ -62,6 +62,52 @@ static inline void st(uint8_t *p, ecc_v v)
     *(ecc_vu *)p = v;
 }
 
+/* Streaming store of a finished plane (nt: the call's outputs exceed the
+ * caches, and every output base is 64-byte aligned): a regular store of a
+ * line that is not in cache first reads it (read-for-ownership), so a
+ * DRAM-bound call moved its outputs twice.  The caller fences (ecc_nt_fence)
+ * before it returns. */
+static inline void stv(uint8_t *p, ecc_v v, int nt)
+{
+#if defined(__AVX512F__)
+    if (nt) {
+        _mm512_stream_si512((__m512i *)(void *)p, (__m512i)v);
+        return;
+    }
+#endif
+    st(p, v);
+}
+
+/* ECC_NT_BYTES: outputs of at least this many bytes per call are streamed */
+#define ECC_NT_BYTES (16u << 20)
+
+static void nt_fence(int nt)
+{
+#if defined(__AVX512F__)
+    if (nt)
+        _mm_sfence();
+#else
+    (void)nt;
+#endif
+}
+
+static int nt_ok(uint8_t *const *out, uint32_t n, uint64_t bytes)
+{
+#if defined(__AVX512F__)
+    if (bytes < ECC_NT_BYTES)
+        return 0;
+    for (uint32_t i = 0; i < n; i++)
+        if ((uintptr_t)out[i] & 63)
+            return 0;
+    return 1;
+#else
+    (void)out;
+    (void)n;
+    (void)bytes;
+    return 0;
+#endif
+}
+
 typedef void (*ecc_fn)(uint8_t *dst, const uint8_t *src);
 
 #define ECGF_X(b) x[b]
@@ -100,7 +146,7 @@ typedef void (*ecc_fn)(uint8_t *dst, const uint8_t *src);
 /* a whole encode row with v = c, the accumulator kept in registers:
  * out = Horner over the k chunks of one stripe (ec_code_c_linear) */
 #define ECC_DEF_ROW(c)                                                         \
-    static void row_##c(uint8_t *out, const uint8_t *in, uint32_t k)           \
+    static void row_##c(uint8_t *out, const uint8_t *in, uint32_t k, int nt)   \
     {                                                                          \
         ecc_v x[8], a[8];                                                      \
         _Pragma("GCC unroll 8") for (int i = 0; i < 8; i++)                    \
@@ -114,7 +160,7 @@ typedef void (*ecc_fn)(uint8_t *dst, const uint8_t *src);
                 x[i] = a[i];                                                   \
         }                                                                      \
         _Pragma("GCC unroll 8") for (int i = 0; i < 8; i++)                    \
-            st(out + 64 * i, x[i]);                                            \
+            stv(out + 64 * i, x[i], nt);                                       \
     }
 ECGF_FOR_EACH(ECC_DEF_MUL)
 ECGF_FOR_EACH(ECC_DEF_MAC)
@@ -127,7 +173,7 @@ ECC_ROWS(ECC_DEF_ROW)
 #define ECC_ENTRY_MAC(c) [c] = mac_##c,
 static const ecc_fn mul_tab[256] = {ECGF_FOR_EACH(ECC_ENTRY_MUL)};
 static const ecc_fn mac_tab[256] = {ECGF_FOR_EACH(ECC_ENTRY_MAC)};
-typedef void (*ecc_row_fn)(uint8_t *out, const uint8_t *in, uint32_t k);
+typedef void (*ecc_row_fn)(uint8_t *out, const uint8_t *in, uint32_t k, int nt);
 #define ECC_ENTRY_ROW(c) [c] = row_##c,
 /* rows of volumes up to EC_MAX_NODES = 31 bricks (ec.h:27-32) */
 static const ecc_row_fn row_tab[32] = {ECC_ROWS(ECC_ENTRY_ROW)};
@@ -138,13 +184,15 @@ static const ecc_row_fn row_tab[32] = {ECC_ROWS(ECC_ENTRY_ROW)};
 void ECC_NAME(ecc_encode)(uint32_t k, uint32_t n, uint64_t nstripes, const uint8_t *in,
                           uint64_t in_stride, uint8_t *const *out, uint64_t out_off)
 {
+    const int nt = nt_ok(out, n, nstripes * 512u * n);
     for (uint64_t t = 0; t < nstripes; t++) {
         const uint8_t *s = in + t * in_stride;
         for (uint32_t i = 0; i < n; i++) {
             uint8_t *o = out[i] + (out_off + t) * 512u;
-            row_tab[i + 1](o, s, k); /* n <= 31: ec_method_init */
+            row_tab[i + 1](o, s, k, nt); /* n <= 31: ec_method_init */
         }
     }
+    nt_fence(nt);
 }
 
 #if defined(__AVX512F__)
@@ -159,7 +207,7 @@ void ECC_NAME(ecc_encode)(uint32_t k, uint32_t n, uint64_t nstripes, const uint8
         ECGF_PROG_##c                                                          \
     } break;
 static void combine_row_reg(uint8_t *o, const uint8_t *const *xp, const uint8_t *coef,
-                            uint32_t k)
+                            uint32_t k, int nt)
 {
     ecc_v a[8] = {{0}};
     for (uint32_t p = 0; p < k; p++) {
@@ -174,7 +222,7 @@ static void combine_row_reg(uint8_t *o, const uint8_t *const *xp, const uint8_t 
         }
     }
     _Pragma("GCC unroll 8") for (int i = 0; i < 8; i++)
-        st(o + 64 * i, a[i]);
+        stv(o + 64 * i, a[i], nt);
 }
 #undef ECC_CASE
 #endif
@@ -186,6 +234,10 @@ void ECC_NAME(ecc_combine)(const ecd_combine_desc_t *d, const uint8_t *pats, uin
                            uint64_t s1)
 {
     const uint32_t k = d->k;
+#if defined(__AVX512F__)
+    const int nt = nt_ok((uint8_t *const *)d->out_base, d->rows,
+                         (s1 - s0) * 512u * d->rows) && !(d->out_stride & 63);
+#endif
     for (uint64_t t = s0; t < s1; t++) {
         uint32_t q = 0;
         if (d->group_pattern) {
@@ -200,7 +252,7 @@ void ECC_NAME(ecc_combine)(const ecd_combine_desc_t *d, const uint8_t *pats, uin
             xs[p] = (const uint8_t *)d->in_base[pat[p]] + t * d->in_stride;
         for (uint32_t r = 0; r < d->rows; r++)
             combine_row_reg((uint8_t *)d->out_base[r] + t * d->out_stride, xs,
-                            pat + k + (size_t)r * k, k);
+                            pat + k + (size_t)r * k, k, nt);
         continue;
 #endif
         for (uint32_t r = 0; r < d->rows; r++) {
@@ -222,4 +274,7 @@ void ECC_NAME(ecc_combine)(const ecd_combine_desc_t *d, const uint8_t *pats, uin
                 memset(o, 0, 512);
         }
     }
+#if defined(__AVX512F__)
+    nt_fence(nt);
+#endif
 }

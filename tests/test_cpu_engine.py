@@ -189,3 +189,29 @@ def test_every_constant_first_and_later_terms(ec, oracle, gen):
             if len(first) == 255 and len(later) == 255:
                 break
     assert len(first) == 255 and len(later) == 255, (len(first), len(later))
+
+
+@pytest.mark.parametrize("gen", ["avx512"])
+def test_large_calls_stream_outputs(ec, oracle, gen):
+    """Calls whose outputs reach 16 MiB store them with streaming stores
+    (AVX-512, 64-byte-aligned output bases; ec_cpu_kern.c stv): encode, full
+    decode and a heal at that size, and a misaligned output base (regular
+    stores), all bit-exact against the oracle."""
+    _isa_ok(ec, gen)
+    k, n = 4, 6
+    nst = (16 << 20) // (CHUNK * k) + 3                  # > 16 MiB of decode output
+    data = rnd(CHUNK * k * nst, seed=91)
+    want = oracle.encode(k, n, data, nthreads=8)
+    with ec.ECMatrixList(k, n, gen=gen) as L:
+        frags = [np.zeros(CHUNK * nst, np.uint8) for _ in range(n)]
+        L.encode_batch(nst, data, frags)
+        for i in range(n):
+            assert np.array_equal(frags[i], want[i]), i
+        rows = [3, 4, 5, 6]
+        out = np.zeros(data.size, np.uint8)
+        L.decode_batch(nst, 0x3C, rows, [want[r - 1] for r in rows], out)
+        assert np.array_equal(out, data)
+        raw = np.zeros(data.size + 64, np.uint8)
+        odd = raw[8:8 + data.size]
+        L.decode_batch(nst, 0x3C, rows, [want[r - 1] for r in rows], odd)
+        assert np.array_equal(odd, data)
