@@ -194,9 +194,9 @@ def test_every_constant_first_and_later_terms(ec, oracle, gen):
 @pytest.mark.parametrize("gen", ["avx512"])
 def test_large_calls_stream_outputs(ec, oracle, gen):
     """Calls whose outputs reach 16 MiB store them with streaming stores
-    (AVX-512, 64-byte-aligned output bases; ec_cpu_kern.c stv): encode, full
-    decode and a heal at that size, and a misaligned output base (regular
-    stores), all bit-exact against the oracle."""
+    (AVX-512, 64-byte-aligned output bases; ec_cpu_kern.c stv): encode and
+    full decode at that size, and a misaligned output base (regular stores),
+    all bit-exact against the oracle."""
     _isa_ok(ec, gen)
     k, n = 4, 6
     nst = (16 << 20) // (CHUNK * k) + 3                  # > 16 MiB of decode output

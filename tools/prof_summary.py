@@ -68,6 +68,10 @@ def main():
     gib = {"dec_4p2_3C": 1, "enc_4p2": 1, "enc_8p4": 0.25, "dec_8p4_FF0": 0.25,
            "enc_16p4": 2, "dec_8p4_EB5": 0.25, "dec_4p2_0F": 1, "mixed_8p4": 1, "heal_8p4": 1,
            "dec_16p4_FFFF0": 1, "mixed_16p4_64": 1, "rmw_4p2": 1}
+    # overrides: PROF_GIB="dec_8p4_FF0=1,..." (a config profiled at another size)
+    for kv in filter(None, os.environ.get("PROF_GIB", "").split(",")):
+        name, val = kv.split("=")
+        gib[name] = float(val)
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     lines = ["# rocprofv3 summary (%s)" % os.path.basename(src.rstrip("/")), "",
              "| config | kernel | calls | avg us | user GB/s | algorithmic GB/s | HBM frac "
