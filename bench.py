@@ -794,7 +794,9 @@ def bind_rank(g, dev_index, local_world):
     16 CPUs for all ranks together).  Returns what was applied."""
     from glusterfs_amd.dist import bind_to_node
     node = g.device_numa_node(dev_index)
-    cpus = bind_to_node(node)
+    # EC_BENCH_NOBIND=1: leave the affinity alone (diagnosis of placement effects)
+    cpus = (os.sched_getaffinity(0) if os.environ.get("EC_BENCH_NOBIND") == "1"
+            else bind_to_node(node))
     hc = host_cpus()
     share = max(1, hc["threads"] // max(1, local_world))
     os.environ.setdefault("EC_COPY_THREADS", str(min(8, share)))

@@ -5,9 +5,10 @@
  * Shipped configuration (r03; one-process A/Bs in tools/kbench/kb3.hip,
  * profiles/kb3_r03*.log, and round 1-2's tools/kbench/kbench.hip):
  *   encode   4+2, 8+4: narrow-tile encoders (ec_encode_tile_t, 4-stripe
- *            tiles, per-wave 2 KiB row runs); 16+4: the 8-stripe tile
- *            encoder; 2+1, misaligned inputs and pinned-host (zero-copy)
- *            calls: the register-resident ec_encode_vander
+ *            tiles, per-wave 2 KiB row runs); 16+4: the row-group encoder
+ *            (ec_encode_tile_rb, 2 rows per wave); 2+1, misaligned inputs
+ *            and pinned-host (zero-copy) calls: the register-resident
+ *            ec_encode_vander
  *   combine  k <= 8 (decode, heal, mixed, sorted slots, device pattern
  *            table): the narrow-tile ec_combine_n, 4 or 8 waves; k > 8: the
  *            8-stripe ec_combine, 16 waves (two blocks fill a CU's 32 wave
@@ -120,39 +121,6 @@ int ecdk_has_vander(uint32_t k, uint32_t n)
            (k == 16 && n == 20);
 }
 
-namespace {
-
-/* Device-resident encodes through the tile kernels (LDS-DMA staging of 8
- * stripes, one row per wave item, NT stores). Same-box kbench A/B against
- * the register-resident ec_encode_vander (profiles/kbench_r02s.log,
- * kbench_r02t.log, kbench_r02t_q.log = 0.25 GiB):
- *   4+2   through ec_combine's jump-table multiply, 16 waves:
- *         1 GiB 0.494 -> 0.453 ms, 0.25 GiB 0.128 -> 0.111 ms;
- *   8+4   ec_encode_tile, direct products (no Horner chain), 16 waves:
- *         1 GiB 0.514 -> 0.459 ms; at 0.25 GiB (64K-stripe batches) the
- *         register-resident encoder keeps a steadier median (0.126 against
- *         0.143), so batches up to 128K stripes stay there;
- *   16+4  ec_encode_tile, Horner, 1 dword per lane, 16 waves:
- *         1 GiB 0.477 -> 0.446 ms, 0.25 GiB 0.111 -> 0.106 ms. */
-template <int K, int N, int NW, bool DIRECT, int CW>
-int launch_encode_tile(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
-{
-    FragPtrs f;
-    for (int i = 0; i < N; ++i)
-        f.p[i] = static_cast<uint8_t *>(out[i]);
-    const uint64_t g = (nstripes + 7) / 8;
-    if (g == 0)
-        return 0;
-    if (g > 0x7fffffffull)
-        return -EINVAL;
-    hipLaunchKernelGGL((ec_encode_tile<K, N, NW, true, DIRECT, CW>), dim3((u32)g), dim3(NW * 64),
-                       (size_t)K * 8 * ECD_CHUNK, s, static_cast<const uint8_t *>(in), f,
-                       nstripes);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
-}
-
-} // namespace
-
 /* EC_MI355X_ENC=0 keeps the register-resident encoder for every geometry
  * (A/B runs); unset = the tile encoders. */
 static bool enc_tiles()
@@ -186,6 +154,25 @@ int launch_encode_narrow(hipStream_t s, uint64_t nstripes, const void *in, void 
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+/* Row-group encoder (ec_encode_tile_rb): 4-stripe tiles, RB rows per wave,
+ * so the tile is read from LDS N / RB times instead of N times. */
+template <int K, int N, int RB>
+int launch_encode_rb(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
+{
+    FragPtrs f;
+    for (int i = 0; i < N; ++i)
+        f.p[i] = static_cast<uint8_t *>(out[i]);
+    const uint64_t g = (nstripes + 3) / 4;
+    if (g == 0)
+        return 0;
+    if (g > 0x7fffffffull)
+        return -EINVAL;
+    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true>), dim3((u32)g),
+                       dim3((N / RB) * 64), (encode_tile_rb_lds<N, 4, RB, true>(K)), s,
+                       static_cast<const uint8_t *>(in), f, nstripes);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 } // namespace
 
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
@@ -200,14 +187,16 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
      * direct products), 8+4 0.443 -> 0.411 and 64K-stripe batches 0.126 ->
      * 0.095 ms (12 waves, Horner: one row per wave; the 2 KiB row runs also
      * remove the 64-B segment writes of the register encoder, PMC 1.10x);
-     * 16+4 keeps the 8-stripe tile encoder (0.432 against 0.453) */
+     * 16+4: row groups, 2 rows per wave, 10 waves (profiles/r03/
+     * kb3_r03j_rowgroups_ct.log: 1 GiB 0.492 -> 0.401 ms, 32K stripes 0.103
+     * -> 0.092 against the 8-stripe one-row tile encoder) */
     if (!zc && aligned && enc_tiles()) {
         if (k == 4 && n == 6)
             return launch_encode_narrow<4, 6, 6, true>(s, nstripes, in, out);
         if (k == 8 && n == 12)
             return launch_encode_narrow<8, 12, 12, false>(s, nstripes, in, out);
         if (k == 16 && n == 20)
-            return launch_encode_tile<16, 20, 16, false, 1>(s, nstripes, in, out);
+            return launch_encode_rb<16, 20, 2>(s, nstripes, in, out);
     }
     if (k == 2 && n == 3)
         return launch_vander<2, 3, 4>(s, nstripes, in, out, zc);

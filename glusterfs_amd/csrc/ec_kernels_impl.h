@@ -530,6 +530,106 @@ constexpr size_t encode_tile_t_lds(int k)
     return (size_t)k * T * ECD_CHUNK + (WOT ? (size_t)NW * T * ECD_CHUNK : 0);
 }
 
+/* Row-group encoder (r03, for 16+4): one wave item = RB consecutive rows
+ * (v = I0 + 1 .. I0 + RB) for 4 stripes, one dword per plane per lane.  The
+ * item walks the k inputs once and every input plane read from LDS feeds RB
+ * Horner chains, so the tile is read N / RB times instead of N times (the
+ * one-row items of ec_encode_tile read it 20 times at 16+4, PMC: LDS array
+ * ~81 % busy).  Input j + 1 is read while the RB steps of input j run, and
+ * no further (scheduling barriers), which keeps the item at ~8 * (RB + 3)
+ * VGPRs. */
+template <int K, int I0, int RB, int T>
+__device__ __forceinline__ void encode_group_acc(const uint8_t *col, u32 (&acc)[RB][8][1])
+{
+    u32 y[8][1], nx[8][1];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+        y[b][0] = *reinterpret_cast<const u32 *>(col + (u32)b * (T * 64u));
+#pragma unroll
+    for (int q = 0; q < RB; ++q)
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc[q][b][0] = y[b][0];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+        nx[b][0] = *reinterpret_cast<const u32 *>(col + (u32)(T * ECD_CHUNK) + (u32)b * (T * 64u));
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            y[b][0] = nx[b][0];
+        if (j + 1 < K) {
+            const uint8_t *src = col + (u32)(j + 1) * (T * ECD_CHUNK);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                nx[b][0] = *reinterpret_cast<const u32 *>(src + (u32)b * (T * 64u));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<0, RB>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            constexpr u32 v = I0 + q + 1;
+            if constexpr (v == 1) {
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    acc[q][b][0] ^= y[b][0];
+            } else {
+                ecgf::horner<v, 1, true>(acc[q], y);
+            }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+/* T = 4 or 8 stripes per tile (SUB = T / 4 four-stripe sub-tiles), N / RB
+ * row groups, one item per wave: NW = (N / RB) * SUB.  WOT: each row leaves
+ * through the wave's 2 KiB LDS slice as one contiguous 2 KiB run. */
+template <int K, int N, int T, int RB, bool NTS, bool WOT>
+__global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
+    const uint8_t *__restrict__ in, const FragPtrs out, uint64_t nstripes)
+{
+    static_assert(N % RB == 0 && (T == 4 || T == 8), "RB | N, 4- or 8-stripe tiles");
+    constexpr u32 SUB = T / 4, NW = (N / RB) * SUB;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
+        return in + st * (uint64_t)(K * ECD_CHUNK) + p * ECD_CHUNK;
+    }, K, t0, nstripes, wave, lane);
+    __syncthreads();
+    const u32 g = wave / SUB, sub = wave % SUB;
+    const u32 cs = lane >> 4, cc = lane & 15u;
+    const uint64_t s0 = t0 + sub * 4u;          /* first stripe of the sub-tile */
+    const uint8_t *col = lds + (sub * 4u + cs) * 64u + cc * 4u;
+    uint8_t *slice = lds + K * T * ECD_CHUNK + wave * 4u * ECD_CHUNK;
+    static_for<0, N / RB>([&](auto G) {
+        constexpr int I0 = decltype(G)::value * RB;
+        if (g == (u32)decltype(G)::value) {
+            u32 acc[RB][8][1];
+            encode_group_acc<K, I0, RB, T>(col, acc);
+            static_for<0, RB>([&](auto Q) {
+                constexpr int q = decltype(Q)::value;
+                /* the row base by a run-time index: see ec_encode_tile_t */
+                uint8_t *row = out.p[__builtin_amdgcn_readfirstlane(g * RB + q)];
+                if constexpr (WOT) {
+                    store_chunks_via_lds<4, 1, NTS>(slice, acc[q], cs, cc, lane, [&](u32 s) {
+                        return s0 + s < nstripes ? row + (s0 + s) * ECD_CHUNK : nullptr;
+                    });
+                } else if (s0 + cs < nstripes) {
+                    store_chunk<1, NTS>(row + (s0 + cs) * ECD_CHUNK + cc * 4u, acc[q]);
+                }
+            });
+        }
+    });
+}
+
+template <int N, int T, int RB, bool WOT>
+constexpr size_t encode_tile_rb_lds(int k)
+{
+    return (size_t)k * T * ECD_CHUNK + (WOT ? (size_t)(N / RB) * (T / 4) * 4 * ECD_CHUNK : 0);
+}
+
 template <int W>
 inline uint64_t vander_grid(uint64_t nstripes)
 {
@@ -871,7 +971,8 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
  * the row's 4 chunks leave through the wave's LDS slice in 512-B runs (WOT
  * = 2: a half slice, two passes).  PG and SLOTS as in ec_combine (device
  * pattern table; sorted slots, whose runs are padded to 8 and so to 4). */
-template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG = false, bool SLOTS = false>
+template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG = false, bool SLOTS = false,
+          int RB = 1>
 __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
 {
     constexpr u32 T = 4;
@@ -906,22 +1007,30 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
     const uint8_t *col = lds + cs * 64u + cc * 4u;
     uint8_t *slice = lds + k * T * ECD_CHUNK + wave * SLICE;
     const uint64_t ost = slot_stripe<SLOTS>(a, t0 + cs, nslots);
-    for (u32 r = wave; r < a.rows; r += NW) {
-        const u32 rw = a.kw * (1 + r);
-        const u32 w0 = pw.word(a, rw);
-        const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
-        const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
-        const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
-        u32 acc[8][1], y[8][1];
+    /* RB rows per wave item (RB = 2: each input read from LDS feeds two
+     * rows, two copies of the one-dword jump table) */
+    for (u32 r = wave * RB; r < a.rows; r += NW * RB) {
+        uint64_t cl[RB], ch[RB];
+        u32 acc[RB][8][1], y[8][1];
 #pragma unroll
-        for (int b = 0; b < 8; ++b)
-            acc[b][0] = 0;
-        uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
-        uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
-        auto next_c = [&]() {
-            const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
-            cl = (cl >> 8) | (ch << 56);
-            ch >>= 8;
+        for (int q = 0; q < RB; ++q) {
+            const u32 rq = r + q;
+            const bool has = q == 0 || rq < a.rows;     /* wave-uniform */
+            const u32 rw = a.kw * (1 + (has ? rq : r));
+            const u32 w0 = has ? pw.word(a, rw) : 0u;
+            const u32 w1 = K > 4 && has ? pw.word(a, rw + 1) : 0u;
+            const u32 w2 = K > 8 && has ? pw.word(a, rw + 2) : 0u;
+            const u32 w3 = K > 12 && has ? pw.word(a, rw + 3) : 0u;
+            cl[q] = (uint64_t)w0 | ((uint64_t)w1 << 32);
+            ch[q] = (uint64_t)w2 | ((uint64_t)w3 << 32);
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                acc[q][b][0] = 0;
+        }
+        auto next_c = [&](int q) {
+            const u32 c = __builtin_amdgcn_readfirstlane((u32)cl[q] & 0xFFu);
+            cl[q] = (cl[q] >> 8) | (ch[q] << 56);
+            ch[q] >>= 8;
             return c;
         };
         auto load_in = [&](u32 p, u32 (&d)[8][1]) {
@@ -935,19 +1044,36 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
          * input p's multiply; it tied or lost at every k, kb3_r03g.log) */
 #pragma unroll 1
         for (u32 p = 0; p < k; ++p) {
-            const u32 c = next_c();
-            if (c == 0)                  /* ec-code-c.c:11666-11676 */
-                continue;
-            load_in(p, y);
-            ecgf::mul_xor_jt<1>(c, acc, y);
+            if constexpr (RB == 1) {
+                const u32 c = next_c(0);
+                if (c == 0)              /* ec-code-c.c:11666-11676 */
+                    continue;
+                load_in(p, y);
+                ecgf::mul_xor_jt<1>(c, acc[0], y);
+            } else {
+                const u32 c0 = next_c(0), c1 = next_c(1);
+                if ((c0 | c1) == 0)
+                    continue;
+                load_in(p, y);
+                if (c0)
+                    ecgf::mul_xor_jt<1>(c0, acc[0], y);
+                if (c1)
+                    ecgf::mul_xor_jt<1>(c1, acc[1], y);
+            }
         }
-        if constexpr (WOT) {
-            store_chunks_via_lds<T, 1, NTS, WOT>(slice, acc, cs, cc, lane, [&](u32 s) {
-                const uint64_t o = s == cs ? ost : slot_stripe<SLOTS>(a, t0 + s, nslots);
-                return o != kNoSlot ? a.out_base[r] + o * a.out_stride : nullptr;
-            });
-        } else if (ost != kNoSlot) {
-            store_chunk<1, NTS>(a.out_base[r] + ost * a.out_stride + cc * 4u, acc);
+#pragma unroll
+        for (int q = 0; q < RB; ++q) {
+            const u32 rq = r + q;
+            if (q > 0 && rq >= a.rows)
+                break;
+            if constexpr (WOT) {
+                store_chunks_via_lds<T, 1, NTS, WOT>(slice, acc[q], cs, cc, lane, [&](u32 s) {
+                    const uint64_t o = s == cs ? ost : slot_stripe<SLOTS>(a, t0 + s, nslots);
+                    return o != kNoSlot ? a.out_base[rq] + o * a.out_stride : nullptr;
+                });
+            } else if (ost != kNoSlot) {
+                store_chunk<1, NTS>(a.out_base[rq] + ost * a.out_stride + cc * 4u, acc[q]);
+            }
         }
     }
 }

@@ -151,6 +151,106 @@ static void add_tile_t(std::vector<Variant> &v, const char *nm, uint64_t nst, co
                  }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
 }
 
+template <int K, int N, int T, int RB, bool WOT>
+static void add_tile_rb(std::vector<Variant> &v, const char *nm, uint64_t nst, const uint8_t *in,
+                        FragPtrs f)
+{
+    auto kern = ec_encode_tile_rb<K, N, T, RB, true, WOT>;
+    const size_t lds = encode_tile_rb_lds<N, T, RB, WOT>(K);
+    lds_attr((const void *)kern, lds);
+    const uint64_t g = (nst + T - 1) / T;
+    constexpr int NW = (N / RB) * (T / 4);
+    v.push_back({nm, (double)nst * (K + N) * ECD_CHUNK, [=](hipStream_t st) {
+                     hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, in, f, nst);
+                 }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+}
+
+/* Compile-time decode matrix (the kb3 dense coefficients below, c = 1 + (i *
+ * 173 + 11) % 255 for i = r * K + p): how fast would a combine be without the
+ * run-time multiply dispatch (a per-matrix JIT kernel)?  T stripes per tile,
+ * CW = T / 4 dwords per plane per lane, one row per wave item. */
+constexpr u32 ct_coef(int i) { return (u32)(1 + (i * 173 + 11) % 255); }
+
+template <int K, int R, int T>
+__device__ __forceinline__ void ct_row(const uint8_t *col, u32 (&acc)[8][T / 4])
+{
+    constexpr int CW = T / 4;
+    u32 y[8][CW], nx[8][CW];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int w = 0; w < CW; ++w)
+            acc[b][w] = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+        load_plane<CW>(col + (u32)b * (T * 64u), nx[b]);
+    static_for<0, K>([&](auto P) {
+        constexpr int p = decltype(P)::value;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int w = 0; w < CW; ++w)
+                y[b][w] = nx[b][w];
+        if constexpr (p + 1 < K) {
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(col + (u32)(p + 1) * (T * ECD_CHUNK) + (u32)b * (T * 64u), nx[b]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        ecgf::mul_xor<ct_coef(R * K + p), CW, true>(acc, acc, y);
+        __builtin_amdgcn_sched_barrier(0);
+    });
+}
+
+template <int K, int T, int NW, bool WOT>
+__global__ __launch_bounds__(NW * 64) void kb_combine_ct(const CombineArgs a)
+{
+    constexpr int CW = T / 4;
+    constexpr u32 LPS = 16 / CW;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
+        return a.in_base[p] + st * a.in_stride;
+    }, K, t0, a.nstripes, wave, lane);
+    __syncthreads();
+    const u32 cs = lane / LPS, cc = lane % LPS;
+    const uint8_t *col = lds + cs * 64u + cc * (4u * CW);
+    uint8_t *slice = lds + K * T * ECD_CHUNK + wave * T * ECD_CHUNK;
+    for (u32 r = wave; r < (u32)K; r += NW) {
+        const u32 ru = __builtin_amdgcn_readfirstlane(r);
+        static_for<0, K>([&](auto R) {
+            if (ru == (u32)decltype(R)::value) {
+                u32 acc[8][CW];
+                ct_row<K, decltype(R)::value, T>(col, acc);
+                uint8_t *row = a.out_base[ru];
+                if constexpr (WOT) {
+                    store_chunks_via_lds<T, CW, true>(slice, acc, cs, cc, lane, [&](u32 s) {
+                        return t0 + s < a.nstripes ? row + (t0 + s) * a.out_stride : nullptr;
+                    });
+                } else if (t0 + cs < a.nstripes) {
+                    store_chunk<CW, true>(row + (t0 + cs) * a.out_stride + cc * (4u * CW), acc);
+                }
+            }
+        });
+    }
+}
+
+template <int K, int T, int NW, bool WOT>
+static void add_combine_ct(std::vector<Variant> &v, const char *nm, const CombineArgs *a,
+                           double bytes, uint8_t *out, size_t ob)
+{
+    auto kern = kb_combine_ct<K, T, NW, WOT>;
+    const size_t lds = (size_t)K * T * ECD_CHUNK + (WOT ? (size_t)NW * T * ECD_CHUNK : 0);
+    lds_attr((const void *)kern, lds);
+    const uint64_t g = (a->nstripes + T - 1) / T;
+    v.push_back({nm, bytes, [=](hipStream_t st) {
+                     hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, *a);
+                 }, out, ob});
+}
+
 /* decode desc: k inputs (fragments), `rows` outputs, dense coefficients */
 static CombineArgs *make_args(int k, int rows, uint64_t nst, uint8_t *const *frags, uint8_t *out,
                               bool stripe_major, const uint8_t *coef)
@@ -186,11 +286,11 @@ static void add_shipped_combine(std::vector<Variant> &v, const char *nm, const C
                  }, out, ob});
 }
 
-template <int K, int NW, int WOT>
+template <int K, int NW, int WOT, int RB = 1>
 static void add_combine_n(std::vector<Variant> &v, const char *nm, const CombineArgs *a,
                           double bytes, uint8_t *out, size_t ob)
 {
-    auto kern = ec_combine_n<K, NW, false, true, WOT>;
+    auto kern = ec_combine_n<K, NW, false, true, WOT, false, false, RB>;
     const size_t lds = combine_n_lds<NW, WOT>(K);
     lds_attr((const void *)kern, lds);
     const uint64_t g = (a->nstripes + 3) / 4;
@@ -230,6 +330,24 @@ int main(int argc, char **argv)
         run_group("encode 16+4", v, rounds, iters, s);
         v.clear();
     }
+    if (want(groups, "enc16rb")) {
+        for (int big = 0; big < 2; ++big) {
+            const uint64_t nst = big ? user / (16 * ECD_CHUNK) : 32768;
+            FragPtrs f = frag_ptrs(bufB, nst, 20);
+            add_shipped_encode(v, "shipped (tile T8 CW1 NW16)", 16, 20, nst, bufA, f);
+            add_tile_rb<16, 20, 4, 5, true>(v, "RB5 T4 WOT (4 waves)", nst, bufA, f);
+            add_tile_rb<16, 20, 4, 5, false>(v, "RB5 T4 (4 waves)", nst, bufA, f);
+            add_tile_rb<16, 20, 4, 4, true>(v, "RB4 T4 WOT (5 waves)", nst, bufA, f);
+            add_tile_rb<16, 20, 4, 4, false>(v, "RB4 T4 (5 waves)", nst, bufA, f);
+            add_tile_rb<16, 20, 4, 2, true>(v, "RB2 T4 WOT (10 waves)", nst, bufA, f);
+            add_tile_rb<16, 20, 8, 5, true>(v, "RB5 T8 WOT (8 waves)", nst, bufA, f);
+            add_tile_rb<16, 20, 8, 5, false>(v, "RB5 T8 (8 waves)", nst, bufA, f);
+            add_tile_rb<16, 20, 8, 10, false>(v, "RB10 T8 (4 waves)", nst, bufA, f);
+            run_group(big ? "encode 16+4 row groups (size = GiB arg)" : "encode 16+4 row groups, 32K stripes",
+                      v, rounds, iters, s);
+            v.clear();
+        }
+    }
     if (want(groups, "enc8")) {
         for (int big = 0; big < 2; ++big) {
             const uint64_t nst = big ? user / (8 * ECD_CHUNK) : 65536;
@@ -242,6 +360,10 @@ int main(int argc, char **argv)
             add_tile_t<8, 12, 4, 6, false, true>(v, "T4 NW6 WOT", nst, bufA, f);
             add_tile_t<8, 12, 4, 4, false, true>(v, "T4 NW4 WOT", nst, bufA, f);
             add_tile_t<8, 12, 4, 12, false, true>(v, "T4 NW12 WOT", nst, bufA, f);
+            add_tile_rb<8, 12, 4, 2, true>(v, "RB2 T4 WOT (6 waves)", nst, bufA, f);
+            add_tile_rb<8, 12, 4, 3, true>(v, "RB3 T4 WOT (4 waves)", nst, bufA, f);
+            add_tile_rb<8, 12, 4, 4, true>(v, "RB4 T4 WOT (3 waves)", nst, bufA, f);
+            add_tile_rb<8, 12, 8, 3, true>(v, "RB3 T8 WOT (8 waves)", nst, bufA, f);
             run_group(big ? "encode 8+4 (size = GiB arg)" : "encode 8+4, 64K stripes", v, rounds,
                       iters, s);
             v.clear();
@@ -256,6 +378,9 @@ int main(int argc, char **argv)
         add_tile_t<4, 6, 4, 6, false, true>(v, "T4 NW6 WOT", nst, bufA, f);
         add_tile_t<4, 6, 4, 3, true, true>(v, "T4 NW3 direct WOT", nst, bufA, f);
         add_tile_t<4, 6, 4, 3, false, true>(v, "T4 NW3 WOT", nst, bufA, f);
+        add_tile_rb<4, 6, 4, 2, true>(v, "RB2 T4 WOT (3 waves)", nst, bufA, f);
+        add_tile_rb<4, 6, 4, 3, true>(v, "RB3 T4 WOT (2 waves)", nst, bufA, f);
+        add_tile_rb<4, 6, 8, 2, true>(v, "RB2 T8 WOT (6 waves)", nst, bufA, f);
         run_group("encode 4+2", v, rounds, iters, s);
         v.clear();
     }
@@ -276,11 +401,36 @@ int main(int argc, char **argv)
         add_combine_n<K, 8, 0>(v, "narrow NW8", a, bytes, bufB, ob);
         add_combine_n<K, 8, 1>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
         add_combine_n<K, 4, 1>(v, "narrow NW4 WOT", a, bytes, bufB, ob);
+        add_combine_n<K, 8, 1, 2>(v, "narrow NW8 WOT RB2", a, bytes, bufB, ob);
+        add_combine_n<K, 4, 1, 2>(v, "narrow NW4 WOT RB2", a, bytes, bufB, ob);
+        add_combine_n<K, 2, 1, 2>(v, "narrow NW2 WOT RB2", a, bytes, bufB, ob);
+        add_combine_n<K, 8, 0, 2>(v, "narrow NW8 RB2", a, bytes, bufB, ob);
         run_group(title, v, rounds, iters, s);
         v.clear();
     };
     if (want(groups, "dec16"))
         decode_group(std::integral_constant<int, 16>{}, "decode 16+4 dense", false);
+    if (want(groups, "dec16ct")) {  /* compile-time matrix: the JIT question */
+        constexpr int K = 16;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        uint8_t *fr[16];
+        for (int p = 0; p < K; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)ct_coef(i);
+        const CombineArgs *a = make_args(K, K, nst, fr, bufB, true, c);
+        const double bytes = 2.0 * nst * K * ECD_CHUNK;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        add_shipped_combine(v, "shipped (run-time matrix)", a, bytes, bufB, ob);
+        add_combine_ct<K, 8, 16, false>(v, "ct T8 NW16", a, bytes, bufB, ob);
+        add_combine_ct<K, 8, 8, false>(v, "ct T8 NW8", a, bytes, bufB, ob);
+        add_combine_ct<K, 4, 8, true>(v, "ct T4 NW8 WOT", a, bytes, bufB, ob);
+        add_combine_ct<K, 4, 4, true>(v, "ct T4 NW4 WOT", a, bytes, bufB, ob);
+        add_combine_ct<K, 4, 8, false>(v, "ct T4 NW8", a, bytes, bufB, ob);
+        run_group("decode 16+4 dense, compile-time matrix", v, rounds, iters, s);
+        v.clear();
+    }
     if (want(groups, "dec8"))
         decode_group(std::integral_constant<int, 8>{}, "decode 8+4 dense", false);
     if (want(groups, "heal8"))
@@ -365,6 +515,10 @@ int main(int argc, char **argv)
         };
         addm("narrow NW4 WOT", ec_combine_n<K, 4, true, true, 1>, 4, combine_n_lds<4, 1>(K));
         addm("narrow NW8", ec_combine_n<K, 8, true, true, 0>, 8, combine_n_lds<8, 0>(K));
+        addm("narrow NW8 WOT RB2", ec_combine_n<K, 8, true, true, 1, false, false, 2>, 8,
+             combine_n_lds<8, 1>(K));
+        addm("narrow NW4 WOT RB2", ec_combine_n<K, 4, true, true, 1, false, false, 2>, 4,
+             combine_n_lds<4, 1>(K));
         run_group(title, v, rounds, iters, s);
         v.clear();
     };
