@@ -251,6 +251,128 @@ static void add_combine_ct(std::vector<Variant> &v, const char *nm, const Combin
                  }, out, ob});
 }
 
+/* Double-buffered persistent combine for k = 16 (r03 candidate, measured slower: DESIGN.md 3.3.1).  The 8-stripe
+ * tile of ec_combine is split into two 32 KiB halves (inputs 0-7, 8-15) that
+ * stay within the 64 KiB of one block, so two blocks still share a CU, and
+ * the halves are staged one phase ahead of the reads: inputs 8-15 of tile t
+ * land while inputs 0-7 are multiplied, inputs 0-7 of the block's next tile
+ * while inputs 8-15 are.  Synchronisation by counted vmcnt and raw
+ * s_barrier (cdna_hip_programming.md "Pipelining across barriers"): every
+ * wave issues exactly 2 LDS-DMA instructions per half (addresses of missing
+ * stripes are clamped, never skipped) and 8 stores per tile when it has a
+ * row, so
+ *   top of tile t:   outstanding A(t), S(t-1)       -> vmcnt(S) retires A(t)
+ *   after inputs 0-7: outstanding S(t-1), B(t), A(t') -> vmcnt(2 or 0)
+ * and the LDS reads are inline asm (opaque to the compiler, which would
+ * otherwise wait vmcnt(0) before any ds_read behind a pending LDS-DMA).
+ * One p-loop with the half switch at p = 8, so the jump table exists once. */
+template <int NW, bool NTS>
+__global__ __launch_bounds__(NW * 64) void ec_combine_db(const CombineArgs a)
+{
+    static_assert(NW == 16, "16 waves: 2 LDS-DMA instructions per wave per half");
+    constexpr u32 T = 8, K = 16;
+    constexpr u32 HALF = 8 * T * ECD_CHUNK;          /* 32 KiB */
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const uint64_t ntiles = (a.nstripes + T - 1) / T;
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles)
+        return;
+    const uint64_t last = a.nstripes - 1;
+    const PatWords<false> pw(a, 0u, lane, nullptr);
+    /* half h of tile `tile`: input p = 8h + ins / 4, 1 KiB per instruction */
+    auto stage = [&](uint64_t tile, u32 h) {
+#pragma unroll
+        for (u32 j = 0; j < 2; ++j) {
+            const u32 ins = j * NW + wave;
+            const u32 p = h * 8 + ins / 4;
+            const u32 el = (ins % 4) * 64 + lane;
+            const u32 seg = el >> 2;
+            uint64_t st = tile * T + seg % T;
+            st = st < last ? st : last;
+            const uint8_t *g = a.in_base[pw.byte(a, p)] + st * a.in_stride + (seg / T) * 64u +
+                               (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + h * HALF + ins * 1024u), 16, 0, 0);
+        }
+    };
+    const u32 r = wave;
+    const bool has = r < a.rows;                     /* wave-uniform */
+    u32 w[4] = {0u, 0u, 0u, 0u};
+    if (has) {
+        const u32 rw = a.kw * (1 + r);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            w[i] = pw.word(a, rw + i);
+    }
+    const u32 cs = lane >> 3, cc = lane & 7u;
+    const u32 col = (u32)(uintptr_t)lds + cs * 64u + cc * 8u;   /* LDS byte address */
+    stage(t, 0);
+    bool stored = false;
+    for (;;) {
+        if (stored)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        stage(t, 1);
+        const uint64_t tn = t + gridDim.x;
+        const bool more = tn < ntiles;
+        u32 acc[8][2], y[8][2];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc[b][0] = acc[b][1] = 0;
+        uint64_t cl = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        uint64_t ch = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+#pragma unroll 1
+        for (u32 p = 0; p < K; ++p) {
+            if (p == 8) {
+                __builtin_amdgcn_s_barrier();        /* inputs 0-7 read by all */
+                if (more) {
+                    stage(tn, 0);
+                    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_s_barrier();        /* inputs 8-15 landed */
+            }
+            const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+            cl = (cl >> 8) | (ch << 56);
+            ch >>= 8;
+            if (c == 0)                              /* ec-code-c.c:11666-11676 */
+                continue;
+            v4u q0, q1, q2, q3;
+            const u32 addr = col + p * (T * ECD_CHUNK);
+            asm volatile("ds_read2st64_b64 %0, %4 offset1:1\n\t"
+                         "ds_read2st64_b64 %1, %4 offset0:2 offset1:3\n\t"
+                         "ds_read2st64_b64 %2, %4 offset0:4 offset1:5\n\t"
+                         "ds_read2st64_b64 %3, %4 offset0:6 offset1:7\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=v"(q0), "=v"(q1), "=v"(q2), "=v"(q3)
+                         : "v"(addr)
+                         : "memory");
+            y[0][0] = q0.x; y[0][1] = q0.y; y[1][0] = q0.z; y[1][1] = q0.w;
+            y[2][0] = q1.x; y[2][1] = q1.y; y[3][0] = q1.z; y[3][1] = q1.w;
+            y[4][0] = q2.x; y[4][1] = q2.y; y[5][0] = q2.z; y[5][1] = q2.w;
+            y[6][0] = q3.x; y[6][1] = q3.y; y[7][0] = q3.z; y[7][1] = q3.w;
+            ecgf::mul_xor_jt<2>(c, acc, y);
+        }
+        const uint64_t ost = t * T + cs;
+        /* every tile but the grid's last is whole, so a wave with a row
+         * issues its 8 stores (the count the next tile's vmcnt assumes);
+         * lanes of missing stripes (last tile only) store nothing */
+        if (has && ost < a.nstripes)
+            store_chunk<2, NTS>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+        stored = has;
+        if (!more)
+            break;
+        t = tn;
+    }
+}
+
 /* decode desc: k inputs (fragments), `rows` outputs, dense coefficients */
 static CombineArgs *make_args(int k, int rows, uint64_t nst, uint8_t *const *frags, uint8_t *out,
                               bool stripe_major, const uint8_t *coef)
@@ -399,6 +521,18 @@ int main(int argc, char **argv)
         const size_t ob = (size_t)nst * rows * ECD_CHUNK;
         add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
         add_combine_n<K, 8, 0>(v, "narrow NW8", a, bytes, bufB, ob);
+        if constexpr (K == 16) {
+            auto kern = ec_combine_db<16, true>;
+            lds_attr((const void *)kern, 64u << 10);
+            const uint64_t ntiles = (a->nstripes + 7) / 8;
+            for (int per = 1; per <= 3; per += 2) {
+                const uint64_t g = std::min<uint64_t>(ntiles, (uint64_t)per * prop.multiProcessorCount * 2);
+                v.push_back({per == 1 ? "double-buffered halves, 2 blocks/CU" : "double-buffered halves, grid 6/CU",
+                             bytes, [=](hipStream_t st) {
+                                 hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * 16), 64u << 10, st, *a);
+                             }, bufB, ob});
+            }
+        }
         add_combine_n<K, 8, 1>(v, "narrow NW8 WOT", a, bytes, bufB, ob);
         add_combine_n<K, 4, 1>(v, "narrow NW4 WOT", a, bytes, bufB, ob);
         add_combine_n<K, 8, 1, 2>(v, "narrow NW8 WOT RB2", a, bytes, bufB, ob);
@@ -410,6 +544,47 @@ int main(int argc, char **argv)
     };
     if (want(groups, "dec16"))
         decode_group(std::integral_constant<int, 16>{}, "decode 16+4 dense", false);
+    /* Placement of the fragments: contiguous in one allocation (64 MiB apart
+     * at 1 GiB), staggered by p * 4 KiB + p * 64 B, or one hipMalloc each
+     * (as torch tensors are) -- the bench's k >= 8 decodes ran ~8-10 %
+     * slower than kb3's, its 4+2 decode did not. */
+    auto layout_group = [&](auto kk, const char *title) {
+        constexpr int K = decltype(kk)::value;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        const uint64_t fb = nst * ECD_CHUNK;
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)ct_coef(i);
+        const double bytes = 2.0 * nst * K * ECD_CHUNK;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        uint8_t *fr[16];
+        for (int p = 0; p < K; ++p)
+            fr[p] = bufA + (uint64_t)p * fb;
+        add_shipped_combine(v, "contiguous (64 MiB apart at 16+4)", make_args(K, K, nst, fr, bufB, true, c),
+                            bytes, bufB, ob);
+        uint8_t *fs[16];
+        for (int p = 0; p < K; ++p)
+            fs[p] = bufA + (uint64_t)p * fb + (uint64_t)p * (4096 + 64) * 4;
+        add_shipped_combine(v, "staggered by p * 16.25 KiB", make_args(K, K, nst, fs, bufB, true, c),
+                            bytes, bufB, ob);
+        static uint8_t *sep[16];
+        for (int p = 0; p < K; ++p) {
+            CHK(hipMalloc(&sep[p], fb));
+            CHK(hipMemcpy(sep[p], fr[p], fb, hipMemcpyDeviceToDevice));
+        }
+        add_shipped_combine(v, "one hipMalloc per fragment", make_args(K, K, nst, sep, bufB, true, c),
+                            bytes, bufB, ob);
+        run_group(title, v, rounds, iters, s);
+        v.clear();
+        for (int p = 0; p < K; ++p)
+            CHK(hipFree(sep[p]));
+    };
+    if (want(groups, "layout16"))
+        layout_group(std::integral_constant<int, 16>{}, "decode 16+4 dense, fragment placement");
+    if (want(groups, "layout8"))
+        layout_group(std::integral_constant<int, 8>{}, "decode 8+4 dense, fragment placement");
+    if (want(groups, "layout4"))
+        layout_group(std::integral_constant<int, 4>{}, "decode 4+2 dense, fragment placement");
     if (want(groups, "dec16ct")) {  /* compile-time matrix: the JIT question */
         constexpr int K = 16;
         const uint64_t nst = user / (K * ECD_CHUNK);
