@@ -136,9 +136,10 @@ namespace {
 
 /* Narrow-tile encoder (ec_encode_tile_t): 4-stripe tiles, NW waves, each
  * fragment row's 4 chunks stored as one 2 KiB run (tools/kbench/kb3.hip,
- * profiles/kb3_r03*.log). */
-template <int K, int N, int NW, bool DIRECT>
-int launch_encode_narrow(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
+ * profiles/kb3_r03*.log).  RA: byte-aligned input staged through registers
+ * (misaligned device inputs, partial-stripe writes). */
+template <int K, int N, int NW, bool DIRECT, bool RA>
+int launch_encode_narrow(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *out)
 {
     FragPtrs f;
     for (int i = 0; i < N; ++i)
@@ -148,16 +149,15 @@ int launch_encode_narrow(hipStream_t s, uint64_t nstripes, const void *in, void 
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    hipLaunchKernelGGL((ec_encode_tile_t<K, N, 4, NW, true, DIRECT, true>), dim3((u32)g),
-                       dim3(NW * 64), (encode_tile_t_lds<4, NW, true>(K)), s,
-                       static_cast<const uint8_t *>(in), f, nstripes);
+    hipLaunchKernelGGL((ec_encode_tile_t<K, N, 4, NW, true, DIRECT, true, RA>), dim3((u32)g),
+                       dim3(NW * 64), (encode_tile_t_lds<4, NW, true>(K)), s, src, f, nstripes);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 /* Row-group encoder (ec_encode_tile_rb): 4-stripe tiles, RB rows per wave,
  * so the tile is read from LDS N / RB times instead of N times. */
-template <int K, int N, int RB>
-int launch_encode_rb(hipStream_t s, uint64_t nstripes, const void *in, void *const *out)
+template <int K, int N, int RB, bool RA>
+int launch_encode_rb(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *out)
 {
     FragPtrs f;
     for (int i = 0; i < N; ++i)
@@ -167,10 +167,24 @@ int launch_encode_rb(hipStream_t s, uint64_t nstripes, const void *in, void *con
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true>), dim3((u32)g),
-                       dim3((N / RB) * 64), (encode_tile_rb_lds<N, 4, RB, true>(K)), s,
-                       static_cast<const uint8_t *>(in), f, nstripes);
+    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true, RA>), dim3((u32)g),
+                       dim3((N / RB) * 64), (encode_tile_rb_lds<N, 4, RB, true>(K)), s, src, f,
+                       nstripes);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+/* The shipped tile encoder of a geometry (4+2, 8+4, 16+4), -ENOTSUP else. */
+template <bool RA>
+int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSrc src,
+                 void *const *out)
+{
+    if (k == 4 && n == 6)
+        return launch_encode_narrow<4, 6, 6, true, RA>(s, nstripes, src, out);
+    if (k == 8 && n == 12)
+        return launch_encode_narrow<8, 12, 12, false, RA>(s, nstripes, src, out);
+    if (k == 16 && n == 20)
+        return launch_encode_rb<16, 20, 2, RA>(s, nstripes, src, out);
+    return -ENOTSUP;
 }
 
 } // namespace
@@ -178,10 +192,6 @@ int launch_encode_rb(hipStream_t s, uint64_t nstripes, const void *in, void *con
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                        const void *in, void *const *out, bool zc)
 {
-    /* the tile encoders stage their input by LDS-DMA in 16-byte pieces; an
-     * input at any other alignment (a tensor slice) keeps the
-     * register-resident encoder, whose loads take any byte address */
-    const bool aligned = !((uintptr_t)in & 15);
     /* narrow-tile encoders, kb3 A/B against round 2's encoders (ms per GiB
      * unless noted, profiles/kb3_r03d.log): 4+2 0.438 -> 0.423 (6 waves,
      * direct products), 8+4 0.443 -> 0.411 and 64K-stripe batches 0.126 ->
@@ -189,14 +199,13 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
      * remove the 64-B segment writes of the register encoder, PMC 1.10x);
      * 16+4: row groups, 2 rows per wave, 10 waves (profiles/r03/
      * kb3_r03j_rowgroups_ct.log: 1 GiB 0.492 -> 0.401 ms, 32K stripes 0.103
-     * -> 0.092 against the 8-stripe one-row tile encoder) */
-    if (!zc && aligned && enc_tiles()) {
-        if (k == 4 && n == 6)
-            return launch_encode_narrow<4, 6, 6, true>(s, nstripes, in, out);
-        if (k == 8 && n == 12)
-            return launch_encode_narrow<8, 12, 12, false>(s, nstripes, in, out);
-        if (k == 16 && n == 20)
-            return launch_encode_rb<16, 20, 2>(s, nstripes, in, out);
+     * -> 0.092 against the 8-stripe one-row tile encoder).  They stage by
+     * LDS-DMA in 16-byte pieces; an input at any other alignment (a tensor
+     * slice) is staged through registers instead (RA). */
+    if (!zc && enc_tiles() && ecdk_has_vander(k, n) && k != 2) {
+        const EncSrc src{static_cast<const uint8_t *>(in), nullptr};
+        return ((uintptr_t)in & 15) ? encode_tiles<true>(s, k, n, nstripes, src, out)
+                                    : encode_tiles<false>(s, k, n, nstripes, src, out);
     }
     if (k == 2 && n == 3)
         return launch_vander<2, 3, 4>(s, nstripes, in, out, zc);
@@ -248,6 +257,13 @@ int launch_vander_rmw(hipStream_t s, uint64_t nstripes, const uint8_t *edge,
 int ecdk_encode_vander_rmw(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                            const uint8_t *edge, const uint8_t *user_shift, void *const *out)
 {
+    /* the narrow tile encoders with register staging (r03): the edges from
+     * `edge`, the interior in place at any alignment.  One process, 1 GiB,
+     * interior 3 bytes off (profiles/r03/kb3_r03o_rmw.log): 4+2 0.491 ->
+     * 0.461 ms, 8+4 0.511 -> 0.491; 16+4 keeps the register kernel below
+     * (0.456 against 0.466 for the row-group encoder staged this way) */
+    if (enc_tiles() && (k == 4 || k == 8) && ecdk_has_vander(k, n))
+        return encode_tiles<true>(s, k, n, nstripes, EncSrc{user_shift, edge}, out);
     if (k == 2 && n == 3)
         return launch_vander_rmw<2, 3, 4, 1>(s, nstripes, edge, user_shift, out);
     if (k == 4 && n == 6)

@@ -432,6 +432,83 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+/* Input of the tile encoders.  edge == nullptr, RA = false: stripe t of the
+ * data at in + t * S (16-byte aligned, staged by LDS-DMA).  RA = true (any
+ * byte alignment): `in` may sit at any address; with `edge` set this is the
+ * partial-stripe write of ec_method_writev_encode_device -- stripes 0 and
+ * nstripes - 1 (the boundary stripes merged with the old head / tail
+ * content, gathered aligned by ec_rmw_gather) come from edge + 0 and
+ * edge + S, every interior stripe t from the caller's buffer at in + t * S
+ * (in = user - head), so the interior is never copied. */
+struct EncSrc {
+    const uint8_t *in;
+    const uint8_t *edge;
+};
+
+/* RA staging: the same plane-major tile as stage_tile, through registers --
+ * piece i (16 B) = ((p * 8 + b) * T + s) * 4 + q is 16 bytes at
+ * src(stripe) + (p * 8 + b) * 64 + q * 16, read as the dword-aligned dwords
+ * that cover it (4, or 5 when the source is not dword-aligned: the fifth
+ * holds the last wanted byte, so no load touches a page the range does not)
+ * and funnel-shifted by v_alignbyte_b32, then one ds_write_b128.  LDS-DMA
+ * takes 16-byte-aligned sources only. */
+template <int K, int T, int NW>
+__device__ __forceinline__ void stage_tile_realign(uint8_t *lds, const EncSrc src, uint64_t t0,
+                                                   uint64_t nstripes, u32 wave, u32 lane)
+{
+    constexpr u32 S = K * ECD_CHUNK;
+    constexpr u32 NP = K * 8 * T * 4;                      /* 16-byte pieces */
+    constexpr u32 IT = (NP + NW * 64 - 1) / (NW * 64);
+    const u32 sh_in = (u32)(uintptr_t)src.in & 3u;         /* the interior's shift */
+    u32 d[IT][4];
+    bool ok[IT];
+#pragma unroll
+    for (u32 it = 0; it < IT; ++it) {
+        const u32 i = it * (NW * 64) + wave * 64 + lane;
+        const u32 q = i & 3u, sl = (i >> 2) % T, pb = (i >> 2) / T;
+        const uint64_t st = t0 + sl;
+        ok[it] = i < NP && st < nstripes;
+        if (!ok[it])
+            continue;
+        const bool edge = src.edge && (st == 0 || st == nstripes - 1);
+        const uint8_t *a = edge ? src.edge + (st == 0 ? 0u : S) : src.in + st * S;
+        a += pb * 64u + q * 16u;
+        const u32 sh = edge ? 0u : sh_in;
+        const u32 *al = reinterpret_cast<const u32 *>(__builtin_assume_aligned(a - sh, 4));
+        if (sh == 0) {
+            const v4u v = *reinterpret_cast<const v4u *>(al);
+            d[it][0] = v.x;
+            d[it][1] = v.y;
+            d[it][2] = v.z;
+            d[it][3] = v.w;
+        } else {
+            u32 t[5];
+            __builtin_memcpy(t, al, 20);
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                d[it][w] = __builtin_amdgcn_alignbyte(t[w + 1], t[w], sh);
+        }
+    }
+#pragma unroll
+    for (u32 it = 0; it < IT; ++it)
+        if (ok[it])
+            *reinterpret_cast<v4u *>(lds + (it * (NW * 64) + wave * 64 + lane) * 16u) =
+                v4u{d[it][0], d[it][1], d[it][2], d[it][3]};
+}
+
+template <int K, int T, int NW, bool RA>
+__device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src, uint64_t t0,
+                                                  uint64_t nstripes, u32 wave, u32 lane)
+{
+    if constexpr (RA) {
+        stage_tile_realign<K, T, NW>(lds, src, t0, nstripes, wave, lane);
+    } else {
+        stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
+            return src.in + st * (uint64_t)(K * ECD_CHUNK) + p * ECD_CHUNK;
+        }, K, t0, nstripes, wave, lane);
+    }
+}
+
 /* Write the wave's T chunks (lane (cs, cc) holds column cc of stripe cs, CW
  * dwords per plane) through its LDS slice as contiguous 16-B lane pieces:
  * chunk s goes to dst(s) + [0, 512).  dst(s) = nullptr: no stripe. */
@@ -490,9 +567,8 @@ __device__ __forceinline__ void encode_tile_item(const uint8_t *col, uint8_t *sl
     }
 }
 
-template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT>
-__global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const uint8_t *__restrict__ in,
-                                                            const FragPtrs out,
+template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT, bool RA = false>
+__global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const EncSrc src, const FragPtrs out,
                                                             uint64_t nstripes)
 {
     static_assert(T == 4 || T == 8, "4- or 8-stripe tiles");
@@ -503,9 +579,7 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const uint8_t *__res
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
-        return in + st * (uint64_t)(K * ECD_CHUNK) + p * ECD_CHUNK;
-    }, K, t0, nstripes, wave, lane);
+    stage_encode_tile<K, T, NW, RA>(lds, src, t0, nstripes, wave, lane);
     __syncthreads();
     const u32 cs = lane / LPS, cc = lane % LPS;
     const uint8_t *col = lds + cs * 64u + cc * (4u * CW);
@@ -583,9 +657,9 @@ __device__ __forceinline__ void encode_group_acc(const uint8_t *col, u32 (&acc)[
 /* T = 4 or 8 stripes per tile (SUB = T / 4 four-stripe sub-tiles), N / RB
  * row groups, one item per wave: NW = (N / RB) * SUB.  WOT: each row leaves
  * through the wave's 2 KiB LDS slice as one contiguous 2 KiB run. */
-template <int K, int N, int T, int RB, bool NTS, bool WOT>
+template <int K, int N, int T, int RB, bool NTS, bool WOT, bool RA = false>
 __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
-    const uint8_t *__restrict__ in, const FragPtrs out, uint64_t nstripes)
+    const EncSrc src, const FragPtrs out, uint64_t nstripes)
 {
     static_assert(N % RB == 0 && (T == 4 || T == 8), "RB | N, 4- or 8-stripe tiles");
     constexpr u32 SUB = T / 4, NW = (N / RB) * SUB;
@@ -594,9 +668,7 @@ __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
-        return in + st * (uint64_t)(K * ECD_CHUNK) + p * ECD_CHUNK;
-    }, K, t0, nstripes, wave, lane);
+    stage_encode_tile<K, T, NW, RA>(lds, src, t0, nstripes, wave, lane);
     __syncthreads();
     const u32 g = wave / SUB, sub = wave % SUB;
     const u32 cs = lane >> 4, cc = lane & 15u;

@@ -147,7 +147,7 @@ static void add_tile_t(std::vector<Variant> &v, const char *nm, uint64_t nst, co
     lds_attr((const void *)kern, lds);
     const uint64_t g = (nst + T - 1) / T;
     v.push_back({nm, (double)nst * (K + N) * ECD_CHUNK, [=](hipStream_t st) {
-                     hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, in, f, nst);
+                     hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, EncSrc{in, nullptr}, f, nst);
                  }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
 }
 
@@ -161,7 +161,7 @@ static void add_tile_rb(std::vector<Variant> &v, const char *nm, uint64_t nst, c
     const uint64_t g = (nst + T - 1) / T;
     constexpr int NW = (N / RB) * (T / 4);
     v.push_back({nm, (double)nst * (K + N) * ECD_CHUNK, [=](hipStream_t st) {
-                     hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, in, f, nst);
+                     hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, EncSrc{in, nullptr}, f, nst);
                  }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
 }
 
@@ -452,6 +452,46 @@ int main(int argc, char **argv)
         run_group("encode 16+4", v, rounds, iters, s);
         v.clear();
     }
+    /* partial-stripe writes (ecdk_encode_vander_rmw): interior read in place
+     * at a 3-byte misalignment, edges from an aligned scratch: round-2
+     * register kernel against the tile encoders with register staging */
+    auto rmw_group = [&](auto kk, auto nn, auto ww, const char *title) {
+        constexpr int K = decltype(kk)::value, N = decltype(nn)::value, W = decltype(ww)::value;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        FragPtrs f = frag_ptrs(bufB, nst, N);
+        const uint8_t *edge = bufA + user + 4096;        /* 2 stripes, aligned */
+        const uint8_t *ushift = bufA + 3;                 /* interior at +3 bytes */
+        const double bytes = (double)nst * (K + N) * ECD_CHUNK;
+        v.push_back({"round-2 register kernel (LM=1)", bytes, [=](hipStream_t st) {
+                         hipLaunchKernelGGL((ec_encode_vander_rmw<K, N, W, 1>), dim3((u32)vander_grid<W>(nst)),
+                                            dim3(kBlock), 0, st, edge, ushift, f, nst);
+                     }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+        v.push_back({"shipped (tile encoder, register staging)", bytes, [=](hipStream_t st) {
+                         void *o[ECD_MAX_ROWS];
+                         for (int i = 0; i < N; ++i)
+                             o[i] = f.p[i];
+                         if (ecdk_encode_vander_rmw(st, K, N, nst, edge, ushift, o))
+                             exit(9);
+                     }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+        v.push_back({"aligned encode (shipped, reference point)", bytes, [=](hipStream_t st) {
+                         void *o[ECD_MAX_ROWS];
+                         for (int i = 0; i < N; ++i)
+                             o[i] = f.p[i];
+                         if (ecdk_encode_vander(st, K, N, nst, bufA, o, false))
+                             exit(9);
+                     }, nullptr, 0});
+        run_group(title, v, rounds, iters, s);
+        v.clear();
+    };
+    if (want(groups, "rmw"))
+        rmw_group(std::integral_constant<int, 4>{}, std::integral_constant<int, 6>{},
+                  std::integral_constant<int, 2>{}, "partial write 4+2, interior +3 bytes");
+    if (want(groups, "rmw"))
+        rmw_group(std::integral_constant<int, 8>{}, std::integral_constant<int, 12>{},
+                  std::integral_constant<int, 1>{}, "partial write 8+4, interior +3 bytes");
+    if (want(groups, "rmw"))
+        rmw_group(std::integral_constant<int, 16>{}, std::integral_constant<int, 20>{},
+                  std::integral_constant<int, 1>{}, "partial write 16+4, interior +3 bytes");
     if (want(groups, "enc16rb")) {
         for (int big = 0; big < 2; ++big) {
             const uint64_t nst = big ? user / (16 * ECD_CHUNK) : 32768;
