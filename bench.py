@@ -347,13 +347,16 @@ def frac(nbytes, seconds):
 
 
 def extra_configs(c, steps, warmup):
-    """BASELINE's other configs, each timed like the headline over max(3,
-    steps/2) launches -- after at least EXTRA_WARMUP untimed ones: a 60-launch
+    """BASELINE's other configs, each timed like the headline over max(30,
+    steps) launches (ten launches of a 0.1-0.4 ms kernel left the figure to
+    the box's clock transients: profiles/r03/r03p_kernarg.log, 100 launches of
+    the 8+4 decode ran 7 % faster than the bench's ten) -- after at least
+    EXTRA_WARMUP untimed ones: a 60-launch
     kernel trace (profiles/sustain_r02l.log) shows the 16+4 decode at ~400 us,
     rising to ~515 us around launches 6-12 and settling back to 390-410 us,
     so a short warm-up times that clock transient instead of the kernel."""
     torch = c.torch
-    st = max(3, steps // 2)
+    st = max(30, steps)
     warmup = max(warmup, EXTRA_WARMUP)
     ex = {"copy_calibration_GBps": copy_calibration(torch, c.dev, st),
           "timing": "%d launches after %d warm-up launches per config" % (st, warmup)}
@@ -546,7 +549,7 @@ def dist_configs(c, grp, steps, warmup):
     no data-path collective).  Aggregate user GB/s = all ranks' user bytes x
     steps / max-over-ranks wall time between barriers."""
     torch = c.torch
-    st = max(3, steps // 2)
+    st = max(30, steps)
     warmup = max(warmup, EXTRA_WARMUP)          # as in extra_configs
     W = grp.world
     ex = {"timing": "%d launches after %d warm-up launches per config" % (st, warmup)}

@@ -136,9 +136,9 @@ namespace {
 
 /* Narrow-tile encoder (ec_encode_tile_t): 4-stripe tiles, NW waves, each
  * fragment row's 4 chunks stored as one 2 KiB run (tools/kbench/kb3.hip,
- * profiles/kb3_r03*.log).  RA: byte-aligned input staged through registers
- * (misaligned device inputs, partial-stripe writes). */
-template <int K, int N, int NW, bool DIRECT, bool RA>
+ * profiles/kb3_r03*.log).  SM: staging mode (ec_kernels_impl.h
+ * stage_encode_tile; 1 = partial-stripe write). */
+template <int K, int N, int NW, bool DIRECT, int SM>
 int launch_encode_narrow(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *out)
 {
     FragPtrs f;
@@ -149,14 +149,14 @@ int launch_encode_narrow(hipStream_t s, uint64_t nstripes, EncSrc src, void *con
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    hipLaunchKernelGGL((ec_encode_tile_t<K, N, 4, NW, true, DIRECT, true, RA>), dim3((u32)g),
+    hipLaunchKernelGGL((ec_encode_tile_t<K, N, 4, NW, true, DIRECT, true, SM>), dim3((u32)g),
                        dim3(NW * 64), (encode_tile_t_lds<4, NW, true>(K)), s, src, f, nstripes);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 /* Row-group encoder (ec_encode_tile_rb): 4-stripe tiles, RB rows per wave,
  * so the tile is read from LDS N / RB times instead of N times. */
-template <int K, int N, int RB, bool RA>
+template <int K, int N, int RB, int SM>
 int launch_encode_rb(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *out)
 {
     FragPtrs f;
@@ -167,23 +167,23 @@ int launch_encode_rb(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true, RA>), dim3((u32)g),
+    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true, SM>), dim3((u32)g),
                        dim3((N / RB) * 64), (encode_tile_rb_lds<N, 4, RB, true>(K)), s, src, f,
                        nstripes);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 /* The shipped tile encoder of a geometry (4+2, 8+4, 16+4), -ENOTSUP else. */
-template <bool RA>
+template <int SM>
 int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSrc src,
                  void *const *out)
 {
     if (k == 4 && n == 6)
-        return launch_encode_narrow<4, 6, 6, true, RA>(s, nstripes, src, out);
+        return launch_encode_narrow<4, 6, 6, true, SM>(s, nstripes, src, out);
     if (k == 8 && n == 12)
-        return launch_encode_narrow<8, 12, 12, false, RA>(s, nstripes, src, out);
+        return launch_encode_narrow<8, 12, 12, false, SM>(s, nstripes, src, out);
     if (k == 16 && n == 20)
-        return launch_encode_rb<16, 20, 2, RA>(s, nstripes, src, out);
+        return launch_encode_rb<16, 20, 2, SM>(s, nstripes, src, out);
     return -ENOTSUP;
 }
 
@@ -200,13 +200,11 @@ int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
      * 16+4: row groups, 2 rows per wave, 10 waves (profiles/r03/
      * kb3_r03j_rowgroups_ct.log: 1 GiB 0.492 -> 0.401 ms, 32K stripes 0.103
      * -> 0.092 against the 8-stripe one-row tile encoder).  They stage by
-     * LDS-DMA in 16-byte pieces; an input at any other alignment (a tensor
-     * slice) is staged through registers instead (RA). */
-    if (!zc && enc_tiles() && ecdk_has_vander(k, n) && k != 2) {
-        const EncSrc src{static_cast<const uint8_t *>(in), nullptr};
-        return ((uintptr_t)in & 15) ? encode_tiles<true>(s, k, n, nstripes, src, out)
-                                    : encode_tiles<false>(s, k, n, nstripes, src, out);
-    }
+     * LDS-DMA, which takes any source alignment (a tensor slice at an odd
+     * offset; tools/kbench/ldsdma_align.hip). */
+    if (!zc && enc_tiles() && ecdk_has_vander(k, n) && k != 2)
+        return encode_tiles<0>(s, k, n, nstripes, EncSrc{static_cast<const uint8_t *>(in), nullptr},
+                               out);
     if (k == 2 && n == 3)
         return launch_vander<2, 3, 4>(s, nstripes, in, out, zc);
     if (k == 4 && n == 6)
@@ -257,13 +255,13 @@ int launch_vander_rmw(hipStream_t s, uint64_t nstripes, const uint8_t *edge,
 int ecdk_encode_vander_rmw(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,
                            const uint8_t *edge, const uint8_t *user_shift, void *const *out)
 {
-    /* the narrow tile encoders with register staging (r03): the edges from
-     * `edge`, the interior in place at any alignment.  One process, 1 GiB,
-     * interior 3 bytes off (profiles/r03/kb3_r03o_rmw.log): 4+2 0.491 ->
-     * 0.461 ms, 8+4 0.511 -> 0.491; 16+4 keeps the register kernel below
-     * (0.456 against 0.466 for the row-group encoder staged this way) */
-    if (enc_tiles() && (k == 4 || k == 8) && ecdk_has_vander(k, n))
-        return encode_tiles<true>(s, k, n, nstripes, EncSrc{user_shift, edge}, out);
+    /* the tile encoders (r03): the edges from `edge`, the interior in place
+     * at any alignment, both by LDS-DMA.  One process, 1 GiB, interior 3
+     * bytes off (profiles/r03/kb3_r03q_ldsdma_unaligned.log): 4+2 0.515 ->
+     * 0.453 ms, 8+4 0.545 -> 0.512, 16+4 0.475 -> 0.440 against the
+     * register kernel, which 2+1 keeps */
+    if (enc_tiles() && k != 2 && ecdk_has_vander(k, n))
+        return encode_tiles<1>(s, k, n, nstripes, EncSrc{user_shift, edge}, out);
     if (k == 2 && n == 3)
         return launch_vander_rmw<2, 3, 4, 1>(s, nstripes, edge, user_shift, out);
     if (k == 4 && n == 6)
@@ -661,84 +659,12 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
     return 0;
 }
 
-namespace {
-
-bool inputs_misaligned(const ecd_combine_desc_t *d)
-{
-    for (u32 p = 0; p < ECD_MAX_ROWS; ++p)
-        if (d->in_base[p] && ((uintptr_t)d->in_base[p] & 15))
-            return true;
-    return false;
-}
-
-/* Every combine stages its inputs by LDS-DMA (global_load_lds_dwordx4),
- * 16 bytes per lane: inputs at another alignment (e.g. torch slices at an
- * odd offset) are first copied, stream-ordered, to aligned scratch -- one
- * copy for bases that share a buffer (the stripe-major input of an encode:
- * in_base[p] = in + p * 512), one per base otherwise. */
-template <bool NTS>
-int combine_realigned(hipStream_t s, const ecd_combine_desc_t *d)
-{
-    if (d->in_stride & 15)
-        return -EINVAL;
-    std::unique_ptr<ecd_combine_desc_t> c(new ecd_combine_desc_t(*d));
-    const uint64_t span = d->nstripes ? (d->nstripes - 1) * d->in_stride + ECD_CHUNK : 0;
-    uintptr_t lo = UINTPTR_MAX, hi = 0, mis = 16;
-    uint64_t total = 0;
-    bool same = true;
-    for (u32 p = 0; p < ECD_MAX_ROWS; ++p) {
-        const uintptr_t b = (uintptr_t)d->in_base[p];
-        if (!b || !(b & 15))
-            continue;
-        same &= mis == 16 || mis == (b & 15);
-        mis = b & 15;
-        lo = std::min(lo, b);
-        hi = std::max<uintptr_t>(hi, b + span);
-        total += span;
-    }
-    std::vector<void *> bufs;
-    int rc = 0;
-    auto copy = [&](uintptr_t from, uint64_t n) -> uint8_t * {
-        void *b = nullptr;
-        if (hipMallocAsync(&b, n ? n : 16, s) != hipSuccess) {
-            (void)hipGetLastError();
-            rc = -ENOMEM;
-            return nullptr;
-        }
-        bufs.push_back(b);
-        if (n && hipMemcpyAsync(b, (const void *)from, n, hipMemcpyDeviceToDevice, s) != hipSuccess) {
-            (void)hipGetLastError();
-            rc = -EIO;
-        }
-        return static_cast<uint8_t *>(b);
-    };
-    if (same && hi - lo <= 2 * total) {
-        uint8_t *b = copy(lo, hi - lo);
-        for (u32 p = 0; rc == 0 && p < ECD_MAX_ROWS; ++p) {
-            const uintptr_t a = (uintptr_t)d->in_base[p];
-            if (a && (a & 15))
-                c->in_base[p] = b + (a - lo);
-        }
-    } else {
-        for (u32 p = 0; rc == 0 && p < ECD_MAX_ROWS; ++p) {
-            const uintptr_t a = (uintptr_t)d->in_base[p];
-            if (a && (a & 15))
-                c->in_base[p] = copy(a, span);
-        }
-    }
-    if (rc == 0)
-        rc = combine_any<NTS>(s, c.get());
-    for (void *b : bufs)
-        (void)hipFreeAsync(b, s);
-    return rc;
-}
-
-} // namespace
-
+/* Every combine stages its inputs by LDS-DMA (global_load_lds_dwordx4), which
+ * takes any source alignment (tools/kbench/ldsdma_align.hip,
+ * profiles/r03/ldsdma_align.log): fragments at odd offsets (torch slices)
+ * are read in place.  (Round 2 copied them to aligned scratch first.) */
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
 {
-    if (inputs_misaligned(d))
-        return combine_realigned<true>(s, d);
     return combine_any<true>(s, d);
 }
 

@@ -432,14 +432,15 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-/* Input of the tile encoders.  edge == nullptr, RA = false: stripe t of the
- * data at in + t * S (16-byte aligned, staged by LDS-DMA).  RA = true (any
- * byte alignment): `in` may sit at any address; with `edge` set this is the
- * partial-stripe write of ec_method_writev_encode_device -- stripes 0 and
- * nstripes - 1 (the boundary stripes merged with the old head / tail
- * content, gathered aligned by ec_rmw_gather) come from edge + 0 and
- * edge + S, every interior stripe t from the caller's buffer at in + t * S
- * (in = user - head), so the interior is never copied. */
+/* Input of the tile encoders: stripe t of the data at in + t * S, at any
+ * byte alignment (LDS-DMA honours any source address:
+ * tools/kbench/ldsdma_align.hip, profiles/r03/ldsdma_align.log).  With
+ * `edge` set this is the partial-stripe write of
+ * ec_method_writev_encode_device: stripes 0 and nstripes - 1 (the boundary
+ * stripes merged with the old head / tail content, gathered by
+ * ec_rmw_gather) come from edge + 0 and edge + S, every interior stripe t
+ * from the caller's buffer at in + t * S (in = user - head), so the interior
+ * is never copied. */
 struct EncSrc {
     const uint8_t *in;
     const uint8_t *edge;
@@ -496,15 +497,25 @@ __device__ __forceinline__ void stage_tile_realign(uint8_t *lds, const EncSrc sr
                 v4u{d[it][0], d[it][1], d[it][2], d[it][3]};
 }
 
-template <int K, int T, int NW, bool RA>
+/* SM (staging mode): 0 = LDS-DMA from in; 1 = LDS-DMA, stripes 0 and
+ * nstripes - 1 from edge (partial-stripe writes); 2 = through registers
+ * (stage_tile_realign, r03 A/B: slower than LDS-DMA at every alignment) */
+template <int K, int T, int NW, int SM>
 __device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src, uint64_t t0,
                                                   uint64_t nstripes, u32 wave, u32 lane)
 {
-    if constexpr (RA) {
+    constexpr uint64_t S = (uint64_t)K * ECD_CHUNK;
+    if constexpr (SM == 2) {
         stage_tile_realign<K, T, NW>(lds, src, t0, nstripes, wave, lane);
+    } else if constexpr (SM == 1) {
+        stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
+            const uint8_t *b = st == 0 ? src.edge : st == nstripes - 1 ? src.edge + S
+                                                                       : src.in + st * S;
+            return b + p * ECD_CHUNK;
+        }, K, t0, nstripes, wave, lane);
     } else {
         stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
-            return src.in + st * (uint64_t)(K * ECD_CHUNK) + p * ECD_CHUNK;
+            return src.in + st * S + p * ECD_CHUNK;
         }, K, t0, nstripes, wave, lane);
     }
 }
@@ -567,7 +578,7 @@ __device__ __forceinline__ void encode_tile_item(const uint8_t *col, uint8_t *sl
     }
 }
 
-template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT, bool RA = false>
+template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT, int SM = 0>
 __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const EncSrc src, const FragPtrs out,
                                                             uint64_t nstripes)
 {
@@ -579,7 +590,7 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const EncSrc src, co
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    stage_encode_tile<K, T, NW, RA>(lds, src, t0, nstripes, wave, lane);
+    stage_encode_tile<K, T, NW, SM>(lds, src, t0, nstripes, wave, lane);
     __syncthreads();
     const u32 cs = lane / LPS, cc = lane % LPS;
     const uint8_t *col = lds + cs * 64u + cc * (4u * CW);
@@ -657,7 +668,7 @@ __device__ __forceinline__ void encode_group_acc(const uint8_t *col, u32 (&acc)[
 /* T = 4 or 8 stripes per tile (SUB = T / 4 four-stripe sub-tiles), N / RB
  * row groups, one item per wave: NW = (N / RB) * SUB.  WOT: each row leaves
  * through the wave's 2 KiB LDS slice as one contiguous 2 KiB run. */
-template <int K, int N, int T, int RB, bool NTS, bool WOT, bool RA = false>
+template <int K, int N, int T, int RB, bool NTS, bool WOT, int SM = 0>
 __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
     const EncSrc src, const FragPtrs out, uint64_t nstripes)
 {
@@ -668,7 +679,7 @@ __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    stage_encode_tile<K, T, NW, RA>(lds, src, t0, nstripes, wave, lane);
+    stage_encode_tile<K, T, NW, SM>(lds, src, t0, nstripes, wave, lane);
     __syncthreads();
     const u32 g = wave / SUB, sub = wave % SUB;
     const u32 cs = lane >> 4, cc = lane & 15u;

@@ -466,7 +466,23 @@ int main(int argc, char **argv)
                          hipLaunchKernelGGL((ec_encode_vander_rmw<K, N, W, 1>), dim3((u32)vander_grid<W>(nst)),
                                             dim3(kBlock), 0, st, edge, ushift, f, nst);
                      }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
-        v.push_back({"shipped (tile encoder, register staging)", bytes, [=](hipStream_t st) {
+        if constexpr (K == 16) {
+            auto kern = ec_encode_tile_rb<16, 20, 4, 2, true, true, 2>;
+            const size_t lds = encode_tile_rb_lds<20, 4, 2, true>(16);
+            v.push_back({"tile encoder, register staging (SM=2)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+        } else {
+            constexpr int NW = N;
+            auto kern = ec_encode_tile_t<K, N, 4, NW, true, (K == 4), true, 2>;
+            const size_t lds = encode_tile_t_lds<4, NW, true>(K);
+            v.push_back({"tile encoder, register staging (SM=2)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+        }
+        v.push_back({"shipped (tile encoder, LDS-DMA at +3 bytes)", bytes, [=](hipStream_t st) {
                          void *o[ECD_MAX_ROWS];
                          for (int i = 0; i < N; ++i)
                              o[i] = f.p[i];
@@ -619,6 +635,33 @@ int main(int argc, char **argv)
         for (int p = 0; p < K; ++p)
             CHK(hipFree(sep[p]));
     };
+    /* fragments at an odd address: read in place by LDS-DMA (r03) */
+    auto misdec_group = [&](auto kk, const char *title) {
+        constexpr int K = decltype(kk)::value;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        const uint64_t fb = nst * ECD_CHUNK + 64;
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)ct_coef(i);
+        const double bytes = 2.0 * nst * K * ECD_CHUNK;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        for (int off : {0, 3, 8}) {
+            uint8_t *fr[16];
+            for (int p = 0; p < K; ++p)
+                fr[p] = bufA + (uint64_t)p * fb + off;
+            static char nm[3][48];
+            snprintf(nm[off == 0 ? 0 : off == 3 ? 1 : 2], 48, "fragments at +%d bytes", off);
+            add_shipped_combine(v, nm[off == 0 ? 0 : off == 3 ? 1 : 2],
+                                make_args(K, K, nst, fr, bufB, true, c), bytes, nullptr, ob);
+        }
+        run_group(title, v, rounds, iters, s);
+        v.clear();
+    };
+    if (want(groups, "misdec")) {
+        misdec_group(std::integral_constant<int, 4>{}, "decode 4+2, fragment alignment");
+        misdec_group(std::integral_constant<int, 8>{}, "decode 8+4, fragment alignment");
+        misdec_group(std::integral_constant<int, 16>{}, "decode 16+4, fragment alignment");
+    }
     if (want(groups, "layout16"))
         layout_group(std::integral_constant<int, 16>{}, "decode 16+4 dense, fragment placement");
     if (want(groups, "layout8"))
