@@ -6,9 +6,9 @@
  * profiles/kb3_r03*.log, and round 1-2's tools/kbench/kbench.hip):
  *   encode   4+2, 8+4: narrow-tile encoders (ec_encode_tile_t, 4-stripe
  *            tiles, per-wave 2 KiB row runs); 16+4: the row-group encoder
- *            (ec_encode_tile_rb, 2 rows per wave); 2+1, misaligned inputs
- *            and pinned-host (zero-copy) calls: the register-resident
- *            ec_encode_vander
+ *            (ec_encode_tile_rb, 2 rows per wave), at any input alignment
+ *            (LDS-DMA); 2+1 and pinned-host (zero-copy) calls: the
+ *            register-resident ec_encode_vander
  *   combine  k <= 8 (decode, heal, mixed, sorted slots, device pattern
  *            table): the narrow-tile ec_combine_n, 4 or 8 waves; k > 8: the
  *            8-stripe ec_combine, 16 waves (two blocks fill a CU's 32 wave

@@ -1,9 +1,9 @@
 """Guards on the device paths:
 
 * inputs at any byte alignment: the tile encoders and every combine stage
-  their inputs by LDS-DMA in 16-byte pieces, so a device input at an odd
-  offset (a torch slice) must take the register-resident encoder or an
-  aligned copy -- bit-exact with the oracle either way;
+  their inputs by LDS-DMA in 16-byte pieces, which honours any source
+  address (r03, tools/kbench/ldsdma_align.hip), so a device input at an odd
+  offset (a torch slice) is read in place -- bit-exact with the oracle;
 * the per-thread host-page cache of the pointer classification
   (ec_device.hip ecd_ptr_device) expires, so a recycled address is
   re-queried: counted with EC_MI355X_DEBUG=1 in a child process;

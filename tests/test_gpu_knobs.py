@@ -2,7 +2,7 @@
 the losing instantiations: DESIGN.md 3.4).
 
 EC_MI355X_ENC=0 runs every device encode through the register-resident
-ec_encode_vander (the kernel misaligned inputs and 2+1 use by default);
+ec_encode_vander (the kernel 2+1 uses by default);
 EC_MI355X_PATCACHE=0 uploads the device pattern table of every mixed call
 instead of caching it.  Each runs here in its own process through the C ABI,
 bit-exact against the oracle on device-resident encode, full / partial
