@@ -373,6 +373,68 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_db(const CombineArgs a)
     }
 }
 
+/* Where does the k = 16 decode's time go?  A copy of ec_combine's single-
+ * pattern k = 16 path (8-stripe tile, 16 waves, CW = 2, jump table) with
+ * the HBM sides removable: MODE bit 0 = no staging loads (compute on
+ * whatever the LDS holds), bit 1 = no stores (kept live by an impossible
+ * run-time condition). */
+template <int MODE>
+__global__ __launch_bounds__(16 * 64) void kb_combine_probe(const CombineArgs a)
+{
+    constexpr u32 T = 8, NW = 16, CW = 2, NI = 16 * T * 32 / 64;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const PatWords<false> pw(a, 0u, lane, nullptr);
+    if constexpr (!(MODE & 1)) {
+#pragma unroll
+        for (u32 j = 0; j < NI / NW; ++j) {
+            const u32 ins = j * NW + wave;
+            const u32 p = ins / (T / 2);
+            const u32 el = (ins * 64 + lane) % (T * 32);
+            const u32 s = (el >> 2) % T;
+            const uint64_t st = t0 + s;
+            if (st < a.nstripes) {
+                const uint8_t *g = a.in_base[pw.byte(a, p)] + st * a.in_stride + ((el >> 2) / T) * 64u +
+                                   (el & 3u) * 16u;
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)g,
+                    (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+            }
+        }
+    }
+    __syncthreads();
+    const u32 cs = lane / 8, cc = lane % 8;
+    const u32 r = wave;
+    const uint8_t *col = lds + cs * 64u + cc * 8u;
+    const u32 rw = a.kw * (1 + r);
+    uint64_t cl = (uint64_t)pw.word(a, rw) | ((uint64_t)pw.word(a, rw + 1) << 32);
+    uint64_t ch = (uint64_t)pw.word(a, rw + 2) | ((uint64_t)pw.word(a, rw + 3) << 32);
+    u32 acc[8][CW], y[8][CW];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+        acc[b][0] = acc[b][1] = 0;
+#pragma unroll 1
+    for (u32 p = 0; p < 16; ++p) {
+        const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+        cl = (cl >> 8) | (ch << 56);
+        ch >>= 8;
+        if (c == 0)
+            continue;
+        const uint8_t *src = col + p * (T * ECD_CHUNK);
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+        ecgf::mul_xor_jt<CW>(c, acc, y);
+    }
+    const uint64_t ost = t0 + cs;
+    const bool st_ok = (MODE & 2) ? a.nstripes == 0x123456789ull : ost < a.nstripes;
+    if (st_ok)
+        store_chunk<CW, true>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+}
+
 /* decode desc: k inputs (fragments), `rows` outputs, dense coefficients */
 static CombineArgs *make_args(int k, int rows, uint64_t nst, uint8_t *const *frags, uint8_t *out,
                               bool stripe_major, const uint8_t *coef)
@@ -577,6 +639,20 @@ int main(int argc, char **argv)
         const size_t ob = (size_t)nst * rows * ECD_CHUNK;
         add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
         add_combine_n<K, 8, 0>(v, "narrow NW8", a, bytes, bufB, ob);
+        if constexpr (K == 16) {
+            static const char *pn[4] = {"probe: full (= shipped)", "probe: no staging loads",
+                                        "probe: no stores", "probe: compute only"};
+            const void *kerns[4] = {(const void *)kb_combine_probe<0>, (const void *)kb_combine_probe<1>,
+                                    (const void *)kb_combine_probe<2>, (const void *)kb_combine_probe<3>};
+            for (int m = 0; m < 4; ++m) {
+                const uint64_t g = (a->nstripes + 7) / 8;
+                const void *kern = kerns[m];
+                v.push_back({pn[m], bytes, [=](hipStream_t st) {
+                                 void *args[] = {(void *)a};
+                                 CHK(hipLaunchKernel(kern, dim3((u32)g), dim3(1024), args, 64u << 10, st));
+                             }, m == 0 ? bufB : nullptr, ob});
+            }
+        }
         if constexpr (K == 16) {
             auto kern = ec_combine_db<16, true>;
             lds_attr((const void *)kern, 64u << 10);
