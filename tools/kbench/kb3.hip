@@ -351,7 +351,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_db(const CombineArgs a)
                          "ds_read2st64_b64 %2, %4 offset0:4 offset1:5\n\t"
                          "ds_read2st64_b64 %3, %4 offset0:6 offset1:7\n\t"
                          "s_waitcnt lgkmcnt(0)"
-                         : "=v"(q0), "=v"(q1), "=v"(q2), "=v"(q3)
+                         : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3)
                          : "v"(addr)
                          : "memory");
             y[0][0] = q0.x; y[0][1] = q0.y; y[1][0] = q0.z; y[1][1] = q0.w;
@@ -424,15 +424,57 @@ __global__ __launch_bounds__(16 * 64) void kb_combine_probe(const CombineArgs a)
         if (c == 0)
             continue;
         const uint8_t *src = col + p * (T * ECD_CHUNK);
+        if constexpr (MODE & 4) {
+            /* 8 single ds_read_b64 (2 LDS cycles each) instead of the 4
+             * ds_read2st64_b64 (8 each) the compiler pairs them into */
+            const u32 ad = (u32)(uintptr_t)src;
+            v2u q[8];
+            asm volatile("ds_read_b64 %0, %8\n\t"
+                         "ds_read_b64 %1, %8 offset:512\n\t"
+                         "ds_read_b64 %2, %8 offset:1024\n\t"
+                         "ds_read_b64 %3, %8 offset:1536\n\t"
+                         "ds_read_b64 %4, %8 offset:2048\n\t"
+                         "ds_read_b64 %5, %8 offset:2560\n\t"
+                         "ds_read_b64 %6, %8 offset:3072\n\t"
+                         "ds_read_b64 %7, %8 offset:3584\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]),
+                           "=&v"(q[5]), "=&v"(q[6]), "=&v"(q[7])
+                         : "v"(ad)
+                         : "memory");
 #pragma unroll
-        for (int b = 0; b < 8; ++b)
-            load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+            for (int b = 0; b < 8; ++b) {
+                y[b][0] = q[b].x;
+                y[b][1] = q[b].y;
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                load_plane<CW>(src + (u32)b * (T * 64u), y[b]);
+        }
         ecgf::mul_xor_jt<CW>(c, acc, y);
     }
     const uint64_t ost = t0 + cs;
     const bool st_ok = (MODE & 2) ? a.nstripes == 0x123456789ull : ost < a.nstripes;
-    if (st_ok)
+    if constexpr (MODE & 8) {
+        /* 16-byte stores: lane pairs (cc, cc ^ 1) swap halves so the even
+         * lane holds 16 B of plane b, the odd lane 16 B of plane b + 1 */
+        const bool odd = cc & 1u;
+        uint8_t *o = a.out_base[r] + ost * a.out_stride + (cc & ~1u) * 8u;
+#pragma unroll
+        for (int b = 0; b < 8; b += 2) {
+            const u32 s0 = odd ? acc[b][0] : acc[b + 1][0];
+            const u32 s1 = odd ? acc[b][1] : acc[b + 1][1];
+            const u32 r0 = __builtin_amdgcn_mov_dpp(s0, 0xB1, 0xF, 0xF, false);
+            const u32 r1 = __builtin_amdgcn_mov_dpp(s1, 0xB1, 0xF, 0xF, false);
+            const v4u out = odd ? v4u{r0, r1, acc[b + 1][0], acc[b + 1][1]}
+                                : v4u{acc[b][0], acc[b][1], r0, r1};
+            if (st_ok)
+                __builtin_nontemporal_store(out, reinterpret_cast<v4u *>(o + (b + (odd ? 1 : 0)) * 64));
+        }
+    } else if (st_ok) {
         store_chunk<CW, true>(a.out_base[r] + ost * a.out_stride + cc * 8u, acc);
+    }
 }
 
 /* decode desc: k inputs (fragments), `rows` outputs, dense coefficients */
@@ -640,20 +682,6 @@ int main(int argc, char **argv)
         add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
         add_combine_n<K, 8, 0>(v, "narrow NW8", a, bytes, bufB, ob);
         if constexpr (K == 16) {
-            static const char *pn[4] = {"probe: full (= shipped)", "probe: no staging loads",
-                                        "probe: no stores", "probe: compute only"};
-            const void *kerns[4] = {(const void *)kb_combine_probe<0>, (const void *)kb_combine_probe<1>,
-                                    (const void *)kb_combine_probe<2>, (const void *)kb_combine_probe<3>};
-            for (int m = 0; m < 4; ++m) {
-                const uint64_t g = (a->nstripes + 7) / 8;
-                const void *kern = kerns[m];
-                v.push_back({pn[m], bytes, [=](hipStream_t st) {
-                                 void *args[] = {(void *)a};
-                                 CHK(hipLaunchKernel(kern, dim3((u32)g), dim3(1024), args, 64u << 10, st));
-                             }, m == 0 ? bufB : nullptr, ob});
-            }
-        }
-        if constexpr (K == 16) {
             auto kern = ec_combine_db<16, true>;
             lds_attr((const void *)kern, 64u << 10);
             const uint64_t ntiles = (a->nstripes + 7) / 8;
@@ -744,6 +772,42 @@ int main(int argc, char **argv)
         layout_group(std::integral_constant<int, 8>{}, "decode 8+4 dense, fragment placement");
     if (want(groups, "layout4"))
         layout_group(std::integral_constant<int, 4>{}, "decode 4+2 dense, fragment placement");
+    if (want(groups, "probe16")) {   /* k = 16 decode with its HBM sides removed */
+        constexpr int K = 16;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        uint8_t *fr[16];
+        for (int p = 0; p < K; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)(1 + (i * 173 + 11) % 255);
+        const CombineArgs *a = make_args(K, K, nst, fr, bufB, true, c);
+        const double bytes = 2.0 * nst * K * ECD_CHUNK;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
+        {
+            static const char *pn[10] = {"probe: full (= shipped)", "probe: no staging loads",
+                                        "probe: no stores", "probe: compute only",
+                                        "probe: ds_read_b64 x8", "probe: ds_read_b64 x8, compute only",
+                                        "probe: 16-B stores (DPP pairs)", "probe: b64 reads + 16-B stores",
+                                        "probe: b64 reads, no stores", "probe: 16-B stores, no loads"};
+            const void *kerns[10] = {(const void *)kb_combine_probe<0>, (const void *)kb_combine_probe<1>,
+                                    (const void *)kb_combine_probe<2>, (const void *)kb_combine_probe<3>,
+                                    (const void *)kb_combine_probe<4>, (const void *)kb_combine_probe<7>,
+                                    (const void *)kb_combine_probe<8>, (const void *)kb_combine_probe<12>,
+                                    (const void *)kb_combine_probe<6>, (const void *)kb_combine_probe<9>};
+            for (int m = 0; m < 10; ++m) {
+                const uint64_t g = (a->nstripes + 7) / 8;
+                const void *kern = kerns[m];
+                v.push_back({pn[m], bytes, [=](hipStream_t st) {
+                                 void *args[] = {(void *)a};
+                                 CHK(hipLaunchKernel(kern, dim3((u32)g), dim3(1024), args, 64u << 10, st));
+                             }, (m == 0 || m == 4 || m == 6 || m == 7) ? bufB : nullptr, ob});
+            }
+        }
+        run_group("decode 16+4 dense, probes", v, rounds, iters, s);
+        v.clear();
+    }
     if (want(groups, "dec16ct")) {  /* compile-time matrix: the JIT question */
         constexpr int K = 16;
         const uint64_t nst = user / (K * ECD_CHUNK);
