@@ -60,6 +60,14 @@ typedef u32 v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
 
+/* Cache policy of the LDS-DMA staging loads (aux operand of
+ * global_load_lds: 0 = default, 2 = non-temporal); EC_LDSDMA_AUX overrides
+ * it for A/B builds of the development harness. */
+#ifndef EC_LDSDMA_AUX
+#define EC_LDSDMA_AUX 0
+#endif
+constexpr int kLdsDmaAux = EC_LDSDMA_AUX;
+
 /* Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E). */
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F &&f)
@@ -309,7 +317,7 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile(const uint8_t *__restr
             const uint8_t *g = in + st * S + p * ECD_CHUNK + ((el >> 2) / T) * 64u + (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaAux);
         }
     }
     __syncthreads();
@@ -419,7 +427,7 @@ __device__ __forceinline__ void stage_tile(uint8_t *lds, A chunk, u32 k, uint64_
             const uint8_t *g = c + (seg / T) * 64u + (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaAux);
         }
     }
 }
@@ -1056,7 +1064,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                                (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaAux);
         }
     }
     __syncthreads();
@@ -1280,7 +1288,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
             const uint8_t *g = a.in_base[src] + st * a.in_stride + (e % 32) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, 0);
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaAux);
         }
     }
     __syncthreads();
