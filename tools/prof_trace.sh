@@ -12,10 +12,11 @@ while [ $# -ge 2 ]; do
   NAME=$(echo "$CFG" | tr ':+' '_p')
   echo "[$(date +%T)] $CFG"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/$NAME" -o run --output-format csv -- \
-    python3 "$R/bench.py" --only "$CFG" --gib "$GIB" --steps 10 --warmup 2 > "$OUT/$NAME.log" 2>&1
+    python3 "$R/bench.py" --only "$CFG" --gib "$GIB" --steps ${STEPS:-10} --warmup 2 > "$OUT/$NAME.log" 2>&1
   rc=$?
   echo "rc=$rc"; tail -1 "$OUT/$NAME.log"
   if [ $rc -ne 0 ]; then exit $rc; fi
   python3 "$R/tools/prof_filter.py" "$OUT/$NAME"
   grep -h "ec_" "$OUT/$NAME"/*kernel_stats.csv | cut -c1-200
+  python3 "$R/tools/trace_seq.py" "$OUT/$NAME" > "$OUT/${NAME}_seq.txt"
 done
