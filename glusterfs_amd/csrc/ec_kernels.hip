@@ -16,6 +16,8 @@
  *            multiply by a jump into the searched XOR programs
  *   stores   non-temporal on every device-path kernel except the 2+1 / 4+2
  *            register encoders (profiles/kbench_r01_nts.log)
+ *   staging  LDS-DMA loads non-temporal for calls whose input exceeds the
+ *            MALL, default policy below it (nt_staging)
  *   host     pinned buffers: the zero-copy kernels (ec_combine_zc,
  *            ec_encode_vander_zc), 1 KiB requests over PCIe
  */
@@ -39,7 +41,31 @@
 
 using namespace ecdev;
 
+/* LDS-DMA staging policy override for A/B runs: -1 = by size (shipped),
+ * 0 = default policy always, 2 = non-temporal always.  EC_MI355X_LDSNT=0/1
+ * sets it at load; tools/kbench/kb3.hip sets it directly. */
+int ecdk_ldsnt_override = [] {
+    const char *e = getenv("EC_MI355X_LDSNT");
+    return e && *e ? (*e == '0' ? kLdsDmaDefault : kLdsDmaNT) : -1;
+}();
+
 namespace {
+
+/* Non-temporal staging loads for a call that reads >= 256 MiB (the MALL's
+ * capacity: nothing it reads can still be cached for a later call).  One
+ * process, alternating builds, 3 rounds (profiles/r03/ab_ldsdma_nt_r03x.log),
+ * ms per GiB default -> nt: 4+2 decode 0.357 -> 0.330, 8+4 decode 0.359 ->
+ * 0.336, 16+4 decode 0.384 -> 0.377, encoders 0.4-0.9 % faster; but a
+ * 64K-stripe 8+4 encode, whose 32 MiB input the MALL keeps between calls,
+ * 0.094 -> 0.111 ms (16+4, 32K stripes: 0.090 -> 0.111). */
+constexpr uint64_t kNtStagingBytes = 256ull << 20;
+
+bool nt_staging(uint64_t in_bytes)
+{
+    if (ecdk_ldsnt_override >= 0)
+        return ecdk_ldsnt_override == kLdsDmaNT;
+    return in_bytes >= kNtStagingBytes;
+}
 
 /* hipFuncAttributeMaxDynamicSharedMemorySize is per device: set it once per
  * (kernel, device), for the device current on the launching thread (a
@@ -85,7 +111,7 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
 
 /* The 8-stripe ec_combine (k > 8): single pattern, mixed patterns (kernel
  * arguments or, PG, the device table), or sorted slots (SL). */
-template <int K, int NW, bool NTS, bool SL = false>
+template <int K, int NW, bool NTS, bool SL = false, int LA = kLdsDmaDefault>
 int launch_combine(hipStream_t s, const CombineArgs &a)
 {
     /* sorted slots: every pattern's run may carry up to 7 padding slots */
@@ -97,17 +123,17 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
     const size_t lds = combine_lds<1>(a.k);
     if (a.patg) {
         /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
-        const void *kern = (const void *)ec_combine<K, 1, NW, true, NTS, 2, true, true, 1, SL>;
+        const void *kern = (const void *)ec_combine<K, 1, NW, true, NTS, 2, true, true, 1, SL, 1, LA>;
         if (lds + kPatLdsBytes > (64u << 10) &&
             ensure_lds_limit(kern, (int)(combine_lds<1>(K) + kPatLdsBytes)) != 0)
             return -EIO;
-        hipLaunchKernelGGL((ec_combine<K, 1, NW, true, NTS, 2, true, true, 1, SL>), dim3((u32)g),
+        hipLaunchKernelGGL((ec_combine<K, 1, NW, true, NTS, 2, true, true, 1, SL, 1, LA>), dim3((u32)g),
                            dim3(NW * 64), lds + kPatLdsBytes, s, a);
     } else if (a.group_pattern) {
-        hipLaunchKernelGGL((ec_combine<K, 1, NW, true, NTS, 2, false, true, 1, SL>), dim3((u32)g),
+        hipLaunchKernelGGL((ec_combine<K, 1, NW, true, NTS, 2, false, true, 1, SL, 1, LA>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
     } else {
-        hipLaunchKernelGGL((ec_combine<K, 1, NW, false, NTS, 2, false, true, 1>), dim3((u32)g),
+        hipLaunchKernelGGL((ec_combine<K, 1, NW, false, NTS, 2, false, true, 1, false, 1, LA>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
     }
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
@@ -138,7 +164,7 @@ namespace {
  * fragment row's 4 chunks stored as one 2 KiB run (tools/kbench/kb3.hip,
  * profiles/kb3_r03*.log).  SM: staging mode (ec_kernels_impl.h
  * stage_encode_tile; 1 = partial-stripe write). */
-template <int K, int N, int NW, bool DIRECT, int SM>
+template <int K, int N, int NW, bool DIRECT, int SM, int LA>
 int launch_encode_narrow(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *out)
 {
     FragPtrs f;
@@ -149,14 +175,14 @@ int launch_encode_narrow(hipStream_t s, uint64_t nstripes, EncSrc src, void *con
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    hipLaunchKernelGGL((ec_encode_tile_t<K, N, 4, NW, true, DIRECT, true, SM>), dim3((u32)g),
+    hipLaunchKernelGGL((ec_encode_tile_t<K, N, 4, NW, true, DIRECT, true, SM, LA>), dim3((u32)g),
                        dim3(NW * 64), (encode_tile_t_lds<4, NW, true>(K)), s, src, f, nstripes);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 /* Row-group encoder (ec_encode_tile_rb): 4-stripe tiles, RB rows per wave,
  * so the tile is read from LDS N / RB times instead of N times. */
-template <int K, int N, int RB, int SM>
+template <int K, int N, int RB, int SM, int LA>
 int launch_encode_rb(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *out)
 {
     FragPtrs f;
@@ -167,24 +193,33 @@ int launch_encode_rb(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true, SM>), dim3((u32)g),
+    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true, SM, LA>), dim3((u32)g),
                        dim3((N / RB) * 64), (encode_tile_rb_lds<N, 4, RB, true>(K)), s, src, f,
                        nstripes);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 /* The shipped tile encoder of a geometry (4+2, 8+4, 16+4), -ENOTSUP else. */
+template <int SM, int LA>
+int encode_tiles_la(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSrc src,
+                    void *const *out)
+{
+    if (k == 4 && n == 6)
+        return launch_encode_narrow<4, 6, 6, true, SM, LA>(s, nstripes, src, out);
+    if (k == 8 && n == 12)
+        return launch_encode_narrow<8, 12, 12, false, SM, LA>(s, nstripes, src, out);
+    if (k == 16 && n == 20)
+        return launch_encode_rb<16, 20, 2, SM, LA>(s, nstripes, src, out);
+    return -ENOTSUP;
+}
+
 template <int SM>
 int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSrc src,
                  void *const *out)
 {
-    if (k == 4 && n == 6)
-        return launch_encode_narrow<4, 6, 6, true, SM>(s, nstripes, src, out);
-    if (k == 8 && n == 12)
-        return launch_encode_narrow<8, 12, 12, false, SM>(s, nstripes, src, out);
-    if (k == 16 && n == 20)
-        return launch_encode_rb<16, 20, 2, SM>(s, nstripes, src, out);
-    return -ENOTSUP;
+    return nt_staging(nstripes * k * ECD_CHUNK)
+               ? encode_tiles_la<SM, kLdsDmaNT>(s, k, n, nstripes, src, out)
+               : encode_tiles_la<SM, kLdsDmaDefault>(s, k, n, nstripes, src, out);
 }
 
 } // namespace
@@ -545,7 +580,7 @@ int sorted_slots(hipStream_t s, const CombineArgs &a0, F tiles)
 
 /* ------------------------------------------------ narrow tiles (r03) */
 
-template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG, bool SL>
+template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG, bool SL, int LA>
 int launch_n1(hipStream_t s, const CombineArgs &a, uint64_t g)
 {
     if (g == 0)
@@ -553,25 +588,25 @@ int launch_n1(hipStream_t s, const CombineArgs &a, uint64_t g)
     if (g > 0x7fffffffull)
         return -EINVAL;
     const size_t lds = combine_n_lds<NW, WOT, PG>((int)a.k);
-    hipLaunchKernelGGL((ec_combine_n<K, NW, MIXED, NTS, WOT, PG, SL>), dim3((u32)g),
+    hipLaunchKernelGGL((ec_combine_n<K, NW, MIXED, NTS, WOT, PG, SL, 1, LA>), dim3((u32)g),
                        dim3(NW * 64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 /* one k-bucket: single pattern, mixed, device pattern table, sorted slots */
-template <int K, int NW, int WOT, bool NTS>
+template <int K, int NW, int WOT, bool NTS, int LA>
 int launch_narrow_k(hipStream_t s, const CombineArgs &a)
 {
     if (!a.group_pattern)
-        return launch_n1<K, NW, false, NTS, WOT, false, false>(s, a, (a.nstripes + 3) / 4);
+        return launch_n1<K, NW, false, NTS, WOT, false, false, LA>(s, a, (a.nstripes + 3) / 4);
     if (a.group_shift >= 2)          /* groups of >= 4 stripes: a tile is one pattern's */
-        return a.patg ? launch_n1<K, NW, true, NTS, WOT, true, false>(s, a, (a.nstripes + 3) / 4)
-                      : launch_n1<K, NW, true, NTS, WOT, false, false>(s, a, (a.nstripes + 3) / 4);
+        return a.patg ? launch_n1<K, NW, true, NTS, WOT, true, false, LA>(s, a, (a.nstripes + 3) / 4)
+                      : launch_n1<K, NW, true, NTS, WOT, false, false, LA>(s, a, (a.nstripes + 3) / 4);
     return sorted_slots<NTS>(s, a, [](hipStream_t st, const CombineArgs &b) {
         /* runs padded to multiples of 8 slots: worst case 7 per pattern */
         const uint64_t g = (b.nstripes + 8ull * b.npatterns) / 4 + 1;
-        return b.patg ? launch_n1<K, NW, true, NTS, WOT, true, true>(st, b, g)
-                      : launch_n1<K, NW, true, NTS, WOT, false, true>(st, b, g);
+        return b.patg ? launch_n1<K, NW, true, NTS, WOT, true, true, LA>(st, b, g)
+                      : launch_n1<K, NW, true, NTS, WOT, false, true, LA>(st, b, g);
     });
 }
 
@@ -587,19 +622,19 @@ int launch_narrow_k(hipStream_t s, const CombineArgs &a)
  * against 0.421 at best narrow (8 waves, register stores), mixed 0.395
  * against 0.442.  Groups below a tile (8 stripes for ec_combine, 4 for the
  * narrow tiles) are sorted into slots first. */
-template <bool NTS>
+template <bool NTS, int LA>
 int launch_combine_k(hipStream_t s, const CombineArgs &a)
 {
     if (a.k <= 4)
-        return launch_narrow_k<4, 4, 1, NTS>(s, a);
+        return launch_narrow_k<4, 4, 1, NTS, LA>(s, a);
     if (a.k <= 8)
-        return a.nstripes <= (1u << 17) ? launch_narrow_k<8, 8, 1, NTS>(s, a)
-                                        : launch_narrow_k<8, 4, 1, NTS>(s, a);
+        return a.nstripes <= (1u << 17) ? launch_narrow_k<8, 8, 1, NTS, LA>(s, a)
+                                        : launch_narrow_k<8, 4, 1, NTS, LA>(s, a);
     if (a.group_pattern && a.group_shift < 3)
         return sorted_slots<NTS>(s, a, [](hipStream_t st, const CombineArgs &b) {
-            return launch_combine<16, 16, NTS, true>(st, b);
+            return launch_combine<16, 16, NTS, true, LA>(st, b);
         });
-    return launch_combine<16, 16, NTS>(s, a);
+    return launch_combine<16, 16, NTS, false, LA>(s, a);
 }
 
 /* pack, then launch; -E2BIG from the packer means "use a device table" */
@@ -612,8 +647,15 @@ int combine_any(hipStream_t s, const ecd_combine_desc_t *d)
     PatTableCache::Ref ref;
     if (rc == -E2BIG && d->group_pattern)
         rc = upload_table(s, d, a, &tab, ref);
-    if (rc == 0)
-        rc = launch_combine_k<NTS>(s, a);
+    /* staging policy by the call's input bytes; the host-buffer fallback
+     * (NTS = false: pinned memory over PCIe) keeps the default policy */
+    if (rc == 0) {
+        if constexpr (NTS)
+            rc = nt_staging(a.nstripes * a.k * ECD_CHUNK) ? launch_combine_k<NTS, kLdsDmaNT>(s, a)
+                                                          : launch_combine_k<NTS, kLdsDmaDefault>(s, a);
+        else
+            rc = launch_combine_k<NTS, kLdsDmaDefault>(s, a);
+    }
     if (ref.slot >= 0)
         pat_tables().release(ref, s);
     if (tab)

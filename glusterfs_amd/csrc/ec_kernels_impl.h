@@ -60,13 +60,12 @@ typedef u32 v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
 
-/* Cache policy of the LDS-DMA staging loads (aux operand of
- * global_load_lds: 0 = default, 2 = non-temporal); EC_LDSDMA_AUX overrides
- * it for A/B builds of the development harness. */
-#ifndef EC_LDSDMA_AUX
-#define EC_LDSDMA_AUX 0
-#endif
-constexpr int kLdsDmaAux = EC_LDSDMA_AUX;
+/* Cache policy of the LDS-DMA staging loads: the aux operand of
+ * global_load_lds, 0 = default, 2 = non-temporal.  The kernels take it as a
+ * template parameter LA (default 0, the policy of the 8-stripe ec_encode_tile
+ * and the zero-copy kernels); the launchers pick it per call by input size
+ * (ec_kernels.hip nt_staging). */
+constexpr int kLdsDmaDefault = 0, kLdsDmaNT = 2;
 
 /* Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E). */
 template <int B, int E, typename F>
@@ -317,7 +316,7 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile(const uint8_t *__restr
             const uint8_t *g = in + st * S + p * ECD_CHUNK + ((el >> 2) / T) * 64u + (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaAux);
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaDefault);
         }
     }
     __syncthreads();
@@ -408,7 +407,7 @@ __device__ __forceinline__ void encode_tile_acc(const uint8_t *col, u32 (&acc)[8
 /* Stage the tile's k input chunks (stripes t0 .. t0+T-1, any that exist) into
  * the plane-major LDS tile by LDS-DMA: input p, plane b, stripe s at
  * ((p * 8 + b) * T + s) * 64; a wave instruction fills 1 KiB. */
-template <int T, int NW, typename A>
+template <int T, int NW, int LA = kLdsDmaDefault, typename A>
 __device__ __forceinline__ void stage_tile(uint8_t *lds, A chunk, u32 k, uint64_t t0,
                                            uint64_t nstripes, u32 wave, u32 lane)
 {
@@ -427,7 +426,7 @@ __device__ __forceinline__ void stage_tile(uint8_t *lds, A chunk, u32 k, uint64_
             const uint8_t *g = c + (seg / T) * 64u + (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaAux);
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, LA);
         }
     }
 }
@@ -508,7 +507,7 @@ __device__ __forceinline__ void stage_tile_realign(uint8_t *lds, const EncSrc sr
 /* SM (staging mode): 0 = LDS-DMA from in; 1 = LDS-DMA, stripes 0 and
  * nstripes - 1 from edge (partial-stripe writes); 2 = through registers
  * (stage_tile_realign, r03 A/B: slower than LDS-DMA at every alignment) */
-template <int K, int T, int NW, int SM>
+template <int K, int T, int NW, int SM, int LA = kLdsDmaDefault>
 __device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src, uint64_t t0,
                                                   uint64_t nstripes, u32 wave, u32 lane)
 {
@@ -516,13 +515,13 @@ __device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src
     if constexpr (SM == 2) {
         stage_tile_realign<K, T, NW>(lds, src, t0, nstripes, wave, lane);
     } else if constexpr (SM == 1) {
-        stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
+        stage_tile<T, NW, LA>(lds, [&](u32 p, uint64_t st) {
             const uint8_t *b = st == 0 ? src.edge : st == nstripes - 1 ? src.edge + S
                                                                        : src.in + st * S;
             return b + p * ECD_CHUNK;
         }, K, t0, nstripes, wave, lane);
     } else {
-        stage_tile<T, NW>(lds, [&](u32 p, uint64_t st) {
+        stage_tile<T, NW, LA>(lds, [&](u32 p, uint64_t st) {
             return src.in + st * S + p * ECD_CHUNK;
         }, K, t0, nstripes, wave, lane);
     }
@@ -586,7 +585,8 @@ __device__ __forceinline__ void encode_tile_item(const uint8_t *col, uint8_t *sl
     }
 }
 
-template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT, int SM = 0>
+template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT, int SM = 0,
+          int LA = kLdsDmaDefault>
 __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const EncSrc src, const FragPtrs out,
                                                             uint64_t nstripes)
 {
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const EncSrc src, co
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    stage_encode_tile<K, T, NW, SM>(lds, src, t0, nstripes, wave, lane);
+    stage_encode_tile<K, T, NW, SM, LA>(lds, src, t0, nstripes, wave, lane);
     __syncthreads();
     const u32 cs = lane / LPS, cc = lane % LPS;
     const uint8_t *col = lds + cs * 64u + cc * (4u * CW);
@@ -676,7 +676,7 @@ __device__ __forceinline__ void encode_group_acc(const uint8_t *col, u32 (&acc)[
 /* T = 4 or 8 stripes per tile (SUB = T / 4 four-stripe sub-tiles), N / RB
  * row groups, one item per wave: NW = (N / RB) * SUB.  WOT: each row leaves
  * through the wave's 2 KiB LDS slice as one contiguous 2 KiB run. */
-template <int K, int N, int T, int RB, bool NTS, bool WOT, int SM = 0>
+template <int K, int N, int T, int RB, bool NTS, bool WOT, int SM = 0, int LA = kLdsDmaDefault>
 __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
     const EncSrc src, const FragPtrs out, uint64_t nstripes)
 {
@@ -687,7 +687,7 @@ __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    stage_encode_tile<K, T, NW, SM>(lds, src, t0, nstripes, wave, lane);
+    stage_encode_tile<K, T, NW, SM, LA>(lds, src, t0, nstripes, wave, lane);
     __syncthreads();
     const u32 g = wave / SUB, sub = wave % SUB;
     const u32 cs = lane >> 4, cc = lane & 15u;
@@ -1018,7 +1018,7 @@ __device__ __forceinline__ void store_chunk_pairs(uint8_t *chunk, u32 cc, const 
  * stripes were sorted by pattern into 8-slot tiles (ec_slots_* kernels), and
  * the block reads its tile's stripes from the slot list. */
 template <int K, int TS, int NW, bool MIXED, bool NTS, int CW = 2, bool PG = false,
-          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1>
+          bool CSE = true, int JT = 0, bool SLOTS = false, int PU = 1, int LA = kLdsDmaDefault>
 __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
 {
     constexpr u32 T = 8 * TS;            /* stripes per tile                   */
@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                                (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaAux);
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, LA);
         }
     }
     __syncthreads();
@@ -1132,7 +1132,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
  * = 2: a half slice, two passes).  PG and SLOTS as in ec_combine (device
  * pattern table; sorted slots, whose runs are padded to 8 and so to 4). */
 template <int K, int NW, bool MIXED, bool NTS, int WOT, bool PG = false, bool SLOTS = false,
-          int RB = 1>
+          int RB = 1, int LA = kLdsDmaDefault>
 __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
 {
     constexpr u32 T = 4;
@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
     /* LDS: the k-input tile, NW output slices, then (PG) the pattern */
     const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp), lane,
                           lds + k * T * ECD_CHUNK + NW * SLICE);
-    stage_tile<T, NW>(lds, [&](u32 p, uint64_t slot) -> const uint8_t * {
+    stage_tile<T, NW, LA>(lds, [&](u32 p, uint64_t slot) -> const uint8_t * {
         const uint64_t st = slot_stripe<SLOTS>(a, slot, nslots);
         return st != kNoSlot ? a.in_base[pw.byte(a, p)] + st * a.in_stride : nullptr;
     }, k, t0, SLOTS ? (uint64_t)nslots : a.nstripes, wave, lane);
@@ -1288,7 +1288,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
             const uint8_t *g = a.in_base[src] + st * a.in_stride + (e % 32) * 16u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaAux);
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, kLdsDmaDefault);
         }
     }
     __syncthreads();

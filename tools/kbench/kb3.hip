@@ -507,7 +507,10 @@ static void add_shipped_combine(std::vector<Variant> &v, const char *nm, const C
                                 double bytes, uint8_t *out, size_t ob)
 {
     v.push_back({nm, bytes, [=](hipStream_t st) {
-                     if (launch_combine_k<true>(st, *a))
+                     const int rc = nt_staging(a->nstripes * a->k * ECD_CHUNK)
+                                        ? launch_combine_k<true, kLdsDmaNT>(st, *a)
+                                        : launch_combine_k<true, kLdsDmaDefault>(st, *a);
+                     if (rc)
                          exit(8);
                  }, out, ob});
 }
@@ -924,6 +927,63 @@ int main(int argc, char **argv)
         mixed_group(std::integral_constant<int, 8>{}, 12, 16, "mixed 8+4, 16 patterns, 1024-stripe groups");
     if (want(groups, "mixed16"))
         mixed_group(std::integral_constant<int, 16>{}, 20, 7, "mixed 16+4, 7 patterns, 1024-stripe groups");
+    /* LDS-DMA staging policy (r03): the shipped choice by input size against
+     * the default and the non-temporal policy at every size, same process;
+     * bytes up to the GiB argument */
+    if (want(groups, "ldsnt")) {
+        auto policies = [&](const char *title, std::function<void(hipStream_t)> fn, double bytes,
+                            uint8_t *out, size_t ob) {
+            static const char *nm[3] = {"shipped (policy by size)", "default policy always",
+                                        "non-temporal always"};
+            const int ov[3] = {-1, kLdsDmaDefault, kLdsDmaNT};
+            for (int i = 0; i < 3; ++i) {
+                const int o = ov[i];
+                v.push_back({nm[i], bytes, [=](hipStream_t st) {
+                                 ecdk_ldsnt_override = o;
+                                 fn(st);
+                             }, out, ob});
+            }
+            run_group(title, v, rounds, iters, s);
+            v.clear();
+            ecdk_ldsnt_override = -1;
+        };
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)(1 + (i * 173 + 11) % 255);
+        static char title[64][96];
+        int nt = 0;
+        for (uint64_t mib : {32ull, 128ull, 256ull, 1024ull}) {
+            if ((mib << 20) > user)
+                continue;
+            for (int K : {4, 8, 16}) {
+                const uint64_t nst = (mib << 20) / (K * ECD_CHUNK);
+                uint8_t *fr[16];
+                for (int p = 0; p < K; ++p)
+                    fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+                const CombineArgs *a = make_args(K, K, nst, fr, bufB, true, c);
+                snprintf(title[nt], 96, "staging policy: decode %d+%d, %llu MiB", K, K == 4 ? 2 : 4,
+                         (unsigned long long)mib);
+                policies(title[nt++], [=](hipStream_t st) {
+                    const int rc = nt_staging(a->nstripes * a->k * ECD_CHUNK)
+                                       ? launch_combine_k<true, kLdsDmaNT>(st, *a)
+                                       : launch_combine_k<true, kLdsDmaDefault>(st, *a);
+                    if (rc)
+                        exit(8);
+                }, 2.0 * nst * K * ECD_CHUNK, bufB, (size_t)nst * K * ECD_CHUNK);
+                const int N = K == 4 ? 6 : K == 8 ? 12 : 20;
+                FragPtrs f = frag_ptrs(bufB, nst, N);
+                snprintf(title[nt], 96, "staging policy: encode %d+%d, %llu MiB", K, N - K,
+                         (unsigned long long)mib);
+                policies(title[nt++], [=](hipStream_t st) {
+                    void *o[ECD_MAX_ROWS];
+                    for (int i = 0; i < N; ++i)
+                        o[i] = f.p[i];
+                    if (ecdk_encode_vander(st, K, N, nst, bufA, o, false))
+                        exit(7);
+                }, (double)nst * (K + N) * ECD_CHUNK, f.p[N - 1], (size_t)nst * ECD_CHUNK);
+            }
+        }
+    }
     CHK(hipFree(bufA));
     CHK(hipFree(bufB));
     return 0;
