@@ -17,7 +17,7 @@
  *   stores   non-temporal on every device-path kernel except the 2+1 / 4+2
  *            register encoders (profiles/kbench_r01_nts.log)
  *   staging  LDS-DMA loads non-temporal for calls whose input exceeds the
- *            MALL, default policy below it (nt_staging)
+ *            MALL (256 MiB), default policy up to it (nt_staging)
  *   host     pinned buffers: the zero-copy kernels (ec_combine_zc,
  *            ec_encode_vander_zc), 1 KiB requests over PCIe
  */
@@ -51,20 +51,25 @@ int ecdk_ldsnt_override = [] {
 
 namespace {
 
-/* Non-temporal staging loads for a call that reads >= 256 MiB (the MALL's
- * capacity: nothing it reads can still be cached for a later call).  One
- * process, alternating builds, 3 rounds (profiles/r03/ab_ldsdma_nt_r03x.log),
- * ms per GiB default -> nt: 4+2 decode 0.357 -> 0.330, 8+4 decode 0.359 ->
- * 0.336, 16+4 decode 0.384 -> 0.377, encoders 0.4-0.9 % faster; but a
- * 64K-stripe 8+4 encode, whose 32 MiB input the MALL keeps between calls,
- * 0.094 -> 0.111 ms (16+4, 32K stripes: 0.090 -> 0.111). */
+/* Non-temporal staging loads for a call that reads more than 256 MiB, the
+ * MALL's capacity: none of its input can still be cached when the same data
+ * comes round again, and default-policy allocation only costs.  Below that,
+ * input a previous call (or producer) left in the MALL is hit.  Same process,
+ * shipped / default / nt interleaved (tools/kbench/kb3.hip group ldsnt,
+ * profiles/r03/kb3_r03y_ldsnt.log, kb3_r03z_ldsnt_sizes.log), ms:
+ *   1 GiB    decode 4+2 0.355 -> 0.327, 8+4 0.356 -> 0.334, 16+4 0.388 ->
+ *            0.376; encoders within 0.5 %
+ *   320 MiB  decode 4+2 0.109 -> 0.105, 16+4 0.138 -> 0.129; encoders tie
+ *   256 MiB  default wins: decode 4+2 0.077 vs 0.086, encode 4+2 0.093 vs
+ *            0.107 (a 64K-stripe 8+4 batch is 256 MiB: configs[2])
+ *   <= 128 MiB default wins or ties, except small 4+2 decodes */
 constexpr uint64_t kNtStagingBytes = 256ull << 20;
 
 bool nt_staging(uint64_t in_bytes)
 {
     if (ecdk_ldsnt_override >= 0)
         return ecdk_ldsnt_override == kLdsDmaNT;
-    return in_bytes >= kNtStagingBytes;
+    return in_bytes > kNtStagingBytes;
 }
 
 /* hipFuncAttributeMaxDynamicSharedMemorySize is per device: set it once per

@@ -4,9 +4,11 @@ the losing instantiations: DESIGN.md 3.4).
 EC_MI355X_ENC=0 runs every device encode through the register-resident
 ec_encode_vander (the kernel 2+1 uses by default);
 EC_MI355X_PATCACHE=0 uploads the device pattern table of every mixed call
-instead of caching it.  Each runs here in its own process through the C ABI,
-bit-exact against the oracle on device-resident encode, full / partial
-decode (ragged tiles included) and mixed decode.
+instead of caching it; EC_MI355X_LDSNT=1 stages these small calls with the
+non-temporal LDS-DMA loads that the library uses above 256 MiB of input.
+Each runs here in its own process through the C ABI, bit-exact against the
+oracle on device-resident encode, full / partial decode (ragged tiles
+included) and mixed decode.
 """
 import os
 import subprocess
@@ -69,7 +71,7 @@ for k, n in ((4, 6), (8, 12), (16, 20)):
 print("ok")
 """
 
-KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0")]
+KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1")]
 
 
 @pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])

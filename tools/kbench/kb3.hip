@@ -952,7 +952,12 @@ int main(int argc, char **argv)
             c[i] = (uint8_t)(1 + (i * 173 + 11) % 255);
         static char title[64][96];
         int nt = 0;
-        for (uint64_t mib : {32ull, 128ull, 256ull, 1024ull}) {
+        const char *szs = getenv("KB3_LDSNT_MIB");      /* e.g. "256,384,512,1024" */
+        std::vector<uint64_t> sizes;
+        for (const char *q = szs ? szs : "32,128,256,1024"; *q; q += (*q == ',')) {
+            sizes.push_back(strtoull(q, const_cast<char **>(&q), 10));
+        }
+        for (uint64_t mib : sizes) {
             if ((mib << 20) > user)
                 continue;
             for (int K : {4, 8, 16}) {
