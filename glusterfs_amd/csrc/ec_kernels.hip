@@ -65,6 +65,16 @@ namespace {
  *   <= 128 MiB default wins or ties, except small 4+2 decodes */
 constexpr uint64_t kNtStagingBytes = 256ull << 20;
 
+/* every input base (and the stride) 16-byte aligned: no staging piece
+ * straddles a cache line (see encode_tiles) */
+bool inputs_aligned(const CombineArgs &a)
+{
+    uintptr_t o = (uintptr_t)a.in_stride;
+    for (u32 p = 0; p < ECD_MAX_ROWS; ++p)   /* unused entries are null */
+        o |= (uintptr_t)a.in_base[p];
+    return (o & 15u) == 0;
+}
+
 bool nt_staging(uint64_t in_bytes)
 {
     if (ecdk_ldsnt_override >= 0)
@@ -218,13 +228,20 @@ int encode_tiles_la(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, En
     return -ENOTSUP;
 }
 
+/* Partial-stripe writes (SM = 1) keep the default policy: their interior is
+ * read at the caller's byte alignment, so neighbouring 16-byte pieces share
+ * cache lines, and the non-temporal loads lost there (kb3 ldsnt,
+ * profiles/r03/kb3_r03ac_ldsnt_rmw.log, 1 GiB at +3 bytes: 4+2 0.450 ->
+ * 0.464 ms, 16+4 0.441 -> 0.447); so do misaligned device inputs. */
 template <int SM>
 int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSrc src,
                  void *const *out)
 {
-    return nt_staging(nstripes * k * ECD_CHUNK)
-               ? encode_tiles_la<SM, kLdsDmaNT>(s, k, n, nstripes, src, out)
-               : encode_tiles_la<SM, kLdsDmaDefault>(s, k, n, nstripes, src, out);
+    const bool aligned = ((uintptr_t)src.in & 15u) == 0;
+    if constexpr (SM == 0)
+        if (aligned && nt_staging(nstripes * k * ECD_CHUNK))
+            return encode_tiles_la<SM, kLdsDmaNT>(s, k, n, nstripes, src, out);
+    return encode_tiles_la<SM, kLdsDmaDefault>(s, k, n, nstripes, src, out);
 }
 
 } // namespace
@@ -656,8 +673,9 @@ int combine_any(hipStream_t s, const ecd_combine_desc_t *d)
      * (NTS = false: pinned memory over PCIe) keeps the default policy */
     if (rc == 0) {
         if constexpr (NTS)
-            rc = nt_staging(a.nstripes * a.k * ECD_CHUNK) ? launch_combine_k<NTS, kLdsDmaNT>(s, a)
-                                                          : launch_combine_k<NTS, kLdsDmaDefault>(s, a);
+            rc = nt_staging(a.nstripes * a.k * ECD_CHUNK) && inputs_aligned(a)
+                     ? launch_combine_k<NTS, kLdsDmaNT>(s, a)
+                     : launch_combine_k<NTS, kLdsDmaDefault>(s, a);
         else
             rc = launch_combine_k<NTS, kLdsDmaDefault>(s, a);
     }

@@ -986,6 +986,18 @@ int main(int argc, char **argv)
                     if (ecdk_encode_vander(st, K, N, nst, bufA, o, false))
                         exit(7);
                 }, (double)nst * (K + N) * ECD_CHUNK, f.p[N - 1], (size_t)nst * ECD_CHUNK);
+                /* partial-stripe write: interior 3 bytes off, edges from scratch */
+                const uint8_t *edge = bufA + user + 4096;
+                const uint8_t *ushift = bufA + 3;
+                snprintf(title[nt], 96, "staging policy: partial write %d+%d (+3 B), %llu MiB", K,
+                         N - K, (unsigned long long)mib);
+                policies(title[nt++], [=](hipStream_t st) {
+                    void *o[ECD_MAX_ROWS];
+                    for (int i = 0; i < N; ++i)
+                        o[i] = f.p[i];
+                    if (ecdk_encode_vander_rmw(st, K, N, nst, edge, ushift, o))
+                        exit(9);
+                }, (double)nst * (K + N) * ECD_CHUNK, f.p[N - 1], (size_t)nst * ECD_CHUNK);
             }
         }
     }
