@@ -733,6 +733,26 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
     return combine_any<true>(s, d);
 }
 
+/* EC_MI355X_ZCDB=1: the persistent double-buffered zero-copy combine
+ * (ec_combine_zc_db, candidate) instead of one tile per block. */
+static bool zc_double_buffered()
+{
+    static const bool v = [] {
+        const char *e = getenv("EC_MI355X_ZCDB");
+        return e && *e == '1';
+    }();
+    return v;
+}
+
+static int cu_count()
+{
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        return 256;
+    return n;
+}
+
 /* Host-buffer path: every buffer is pinned host memory read / written over
  * PCIe (ec_device.hip run_pipeline), so the zero-copy combine with whole
  * 1 KiB request runs; default (not non-temporal) stores there, which cost
@@ -752,6 +772,22 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
         return -EINVAL;
     const size_t lds = (size_t)(d->k + d->rows) * 8 * ECD_CHUNK;
     constexpr int NW = 8;
+    const size_t lds_db = (size_t)(2 * d->k + d->rows) * 8 * ECD_CHUNK + 8 * ECD_MAX_ROWS;
+    if (zc_double_buffered() && d->k <= 8 && lds_db <= (128u << 10) + 8 * ECD_MAX_ROWS) {
+        /* persistent, >= 4 tiles per block so its reads of tile i + 1 and
+         * writes of tile i overlap, at most one block per CU */
+        const uint64_t gdb = std::min<uint64_t>(std::max<uint64_t>(g / 4, 1), (uint64_t)cu_count());
+        const void *kern = d->k <= 4 ? (a.group_pattern ? (const void *)ec_combine_zc_db<4, NW, true>
+                                                        : (const void *)ec_combine_zc_db<4, NW, false>)
+                                     : (a.group_pattern ? (const void *)ec_combine_zc_db<8, NW, true>
+                                                        : (const void *)ec_combine_zc_db<8, NW, false>);
+        if (lds_db > (64u << 10) && ensure_lds_limit(kern, (int)((128u << 10) + 8 * ECD_MAX_ROWS)) != 0)
+            return -EIO;
+        void *args[] = {&a};
+        if (hipLaunchKernel(kern, dim3((u32)gdb), dim3(NW * 64), args, lds_db, s) != hipSuccess)
+            return -EIO;
+        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    }
     if (d->k <= 4) {
         if (a.group_pattern)
             hipLaunchKernelGGL((ec_combine_zc<4, NW, true>), dim3((u32)g), dim3(NW * 64), lds, s, a);

@@ -1351,6 +1351,154 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
     }
 }
 
+/* Zero-copy combine, persistent and double-buffered (r03): the same tiles,
+ * request shapes and output order as ec_combine_zc, but each block walks
+ * tiles blockIdx.x, + gridDim.x, ... and issues the staging loads of its
+ * next tile right before the stores of the current one, so reads from and
+ * writes to host memory are in flight together.  In ec_combine_zc every
+ * block of a small call (a 4 MiB 8+4 heal window is 128 tiles, one block
+ * each, all resident at once) reads, then computes, then writes in
+ * lockstep, and the full-duplex link carries one direction at a time.
+ * Per iteration: compute tile i from buf[i & 1] into otile; barrier; stage
+ * tile i + 1 into buf[(i + 1) & 1] (last read in iteration i - 1, before
+ * its barrier); store tile i; wait for both; barrier.  The otile reads are
+ * inline asm: the compiler would otherwise put a vmcnt(0) for the pending
+ * LDS-DMA in front of them and serialise the two directions again.  Raw
+ * s_barrier with explicit waits (no fences: __syncthreads() adds a
+ * vmcnt(0) per barrier, which is wanted only at the end of an iteration).
+ * The row bases live in LDS: a lane-indexed out_base[r] is a vector load
+ * from the kernel arguments, whose vmcnt(0) would wait for the staging too.
+ * LDS = (2k + rows) * 4 KiB + 8 * ECD_MAX_ROWS. */
+__device__ __forceinline__ uint64_t lds_read_u64(const uint8_t *p)
+{
+    uint64_t v;
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(v)
+                 : "v"((u32)(uintptr_t)p)
+                 : "memory");
+    return v;
+}
+
+__device__ __forceinline__ v4u lds_read_b128(const uint8_t *p)
+{
+    v4u v;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(v)
+                 : "v"((u32)(uintptr_t)p)
+                 : "memory");
+    return v;
+}
+
+template <int K, int NW, bool MIXED>
+__global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
+{
+    constexpr u32 T = 8;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 k = a.k, rows = a.rows;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const u32 tb = k * (T * ECD_CHUNK);
+    uint8_t *otile = lds + 2u * tb;
+    const uint64_t ntiles = (a.nstripes + T - 1) / T;
+    const bool stripe_major = a.out_stride == (uint64_t)rows * ECD_CHUNK;
+
+    /* stage tile t into buffer b: wave instruction ins = 1 KiB = stripes
+     * 2q, 2q + 1 of input p (as ec_combine_zc) */
+    auto stage = [&](uint64_t t, u32 b) {
+        const uint64_t t0 = t * T;
+        const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
+        uint8_t *buf = lds + b * tb;
+        const u32 ni = k * (T / 2);
+        for (u32 ins = wave; ins < ni; ins += NW) {
+            const u32 p = ins / (T / 2);
+            const u32 e = (ins % (T / 2)) * 64 + lane;
+            const uint64_t st = t0 + e / 32;
+            if (st < a.nstripes) {
+                const uint8_t *g = a.in_base[pw.byte(a, p)] + st * a.in_stride + (e % 32) * 16u;
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)g,
+                    (__attribute__((address_space(3))) void *)(buf + ins * 1024u), 16, 0,
+                    kLdsDmaDefault);
+            }
+        }
+    };
+
+    uint8_t *obase = otile + rows * (T * ECD_CHUNK);   /* row bases, 8 B each */
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles)
+        return;                 /* block-uniform: every wave leaves together */
+    if (tid < rows)
+        *reinterpret_cast<uint64_t *>(obase + tid * 8u) = (uint64_t)(uintptr_t)a.out_base[tid];
+    stage(t, 0);
+    __builtin_amdgcn_s_waitcnt(0x0070);        /* vmcnt(0) lgkmcnt(0) */
+    __builtin_amdgcn_s_barrier();
+    const u32 cs = lane >> 3, cc = lane & 7u;
+    for (u32 i = 0;; ++i) {
+        const uint64_t t0 = t * T;
+        const uint8_t *buf = lds + (i & 1u) * tb;
+        {
+            const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
+            for (u32 r = wave; r < rows; r += NW) {
+                const uint8_t *col = buf + cs * ECD_CHUNK + cc * 8u;
+                const u32 rw = a.kw * (1 + r);
+                const u32 w0 = pw.word(a, rw);
+                const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+                u32 acc[8][2], y[8][2];
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    acc[b][0] = acc[b][1] = 0;
+                uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+#pragma unroll 1
+                for (u32 p = 0; p < k; ++p) {
+                    const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+                    cl >>= 8;
+                    if (c == 0)          /* ec-code-c.c:11666-11676 */
+                        continue;
+                    const uint8_t *src = col + p * (T * ECD_CHUNK);
+#pragma unroll
+                    for (int b = 0; b < 8; ++b)
+                        load_plane<2>(src + (u32)b * 64u, y[b]);
+                    ecgf::mul_xor_rt<2>(c, acc, y);
+                }
+                uint8_t *o = otile + (r * T + cs) * ECD_CHUNK + cc * 8u;
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);    /* lgkmcnt(0): otile written */
+        __builtin_amdgcn_s_barrier();
+        const uint64_t tn = t + gridDim.x;
+        if (tn < ntiles)
+            stage(tn, (i + 1u) & 1u);
+        const u32 np = rows * T * 32;
+        for (u32 idx = tid; idx < np; idx += NW * 64) {
+            const u32 w = idx % 32;
+            u32 s, r;
+            if (stripe_major) {
+                s = idx / (rows * 32);
+                r = (idx / 32) % rows;
+            } else {
+                r = idx / (T * 32);
+                s = (idx / 32) % T;
+            }
+            const uint64_t ost = t0 + s;
+            const v4u v = lds_read_b128(otile + (r * T + s) * ECD_CHUNK + w * 16u);
+            uint8_t *ob = reinterpret_cast<uint8_t *>(lds_read_u64(obase + r * 8u));
+            /* a global (not flat) store: a flat one would count in lgkmcnt
+             * as well, and the next ds_read's wait would drain it */
+            if (ost < a.nstripes)
+                *(__attribute__((address_space(1))) v4u *)(ob + ost * a.out_stride + w * 16u) = v;
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);    /* vmcnt(0): tile i + 1 landed, stores out */
+        __builtin_amdgcn_s_barrier();
+        if (tn >= ntiles)
+            break;
+        t = tn;
+    }
+}
+
 /* Counting sort of the stripes of a mixed call by pattern id, for pattern
  * groups of 1, 2 or 4 stripes, so the tile kernel gets 8 stripes of one
  * pattern per tile.  Each pattern's run is padded to a multiple of 8 slots

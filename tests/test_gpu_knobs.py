@@ -5,7 +5,9 @@ EC_MI355X_ENC=0 runs every device encode through the register-resident
 ec_encode_vander (the kernel 2+1 uses by default);
 EC_MI355X_PATCACHE=0 uploads the device pattern table of every mixed call
 instead of caching it; EC_MI355X_LDSNT=1 stages these small calls with the
-non-temporal LDS-DMA loads that the library uses above 256 MiB of input.
+non-temporal LDS-DMA loads that the library uses above 256 MiB of input;
+EC_MI355X_ZCDB=1 runs host-buffer combines (k <= 8) through the persistent
+double-buffered zero-copy kernel instead of one tile per block.
 Each runs here in its own process through the C ABI, bit-exact against the
 oracle on device-resident encode, full / partial decode (ragged tiles
 included) and mixed decode.
@@ -68,15 +70,26 @@ for k, n in ((4, 6), (8, 12), (16, 20)):
             rows = O.mask_rows(ms[ids[gi]])
             exp = O.decode(k, rows, [frags[r - 1][gi * span:(gi + 1) * span] for r in rows])
             assert np.array_equal(got[gi * span * k:(gi + 1) * span * k], exp), ("mixed", k, gi)
+        # host buffers (EC_GPU_ALWAYS=1: the zero-copy combine over staged
+        # pinned slots), several tiles per block of the persistent kernel
+        for nst in (5, 1031, 4100):
+            frags = [rb(512 * nst) for _ in range(n)]
+            out = np.empty(512 * k * nst, np.uint8)
+            for m in masks[:4]:
+                rows = O.mask_rows(m)
+                L.decode_batch(nst, m, rows, [frags[r - 1] for r in rows], out)
+                exp = O.decode(k, rows, [frags[r - 1] for r in rows])
+                assert np.array_equal(out, exp), ("host dec", k, n, nst, hex(m))
 print("ok")
 """
 
-KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1")]
+KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1"),
+         ("EC_MI355X_ZCDB", "1")]
 
 
 @pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])
 def test_ab_instantiation_bit_exact(knob, value):
-    env = dict(os.environ, EC_MI355X_QUIET="1")
+    env = dict(os.environ, EC_MI355X_QUIET="1", EC_GPU_ALWAYS="1")
     env[knob] = value
     r = subprocess.run([sys.executable, "-c", SCRIPT], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=110)
