@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -744,12 +745,19 @@ static bool zc_double_buffered()
     return v;
 }
 
+/* CUs of the current device, queried once per device */
 static int cu_count()
 {
+    static std::atomic<int> cus[64];
     int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0)
         return 256;
+    if (dev < 64 && (n = cus[dev].load(std::memory_order_relaxed)) > 0)
+        return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        return 256;
+    if (dev < 64)
+        cus[dev].store(n, std::memory_order_relaxed);
     return n;
 }
 
