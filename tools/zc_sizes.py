@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Host-buffer decode time per call by size (development probe, GPU box):
+8+4 and 4+2 decodes from pinned buffers (ec_method_host_alloc, i.e. the
+zero-copy combine) at 4-256 MiB of user data, median of repeated calls.
+Run once per EC_MI355X_ZCDB setting (read at library load); EC_GPU_ALWAYS=1
+keeps every call on the GPU.  Usage: python tools/zc_sizes.py"""
+import ctypes
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401  (torch first: one HIP runtime)
+import glusterfs_amd as g  # noqa: E402
+
+
+def pinned(lib, nb):
+    p = lib.ec_method_host_alloc(nb)
+    if not p:
+        raise MemoryError
+    return p, np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(p))
+
+
+def main():
+    lib = g.ec_method.lib
+    print("EC_MI355X_ZCDB=%s" % os.environ.get("EC_MI355X_ZCDB", "unset"))
+    for k, n in ((8, 12), (4, 6)):
+        for mib in (4, 16, 64, 256):
+            S = mib << 20
+            nst = S // (512 * k)
+            bufs = []
+            try:
+                din_p, din = pinned(lib, S)
+                bufs.append(din_p)
+                din[:] = np.random.default_rng(mib).integers(0, 256, S, dtype=np.uint8)
+                fr = [pinned(lib, nst * 512) for _ in range(n)]
+                bufs += [p for p, _ in fr]
+                dout_p, dout = pinned(lib, S)
+                bufs.append(dout_p)
+                with g.ECMatrixList(k, n) as L:
+                    L.encode_batch(nst, din_p, [p for p, _ in fr])
+                    rows = list(range(n - k + 1, n + 1))
+                    mask = sum(1 << (r - 1) for r in rows)
+                    ins = [fr[r - 1][0] for r in rows]
+                    L.decode_batch(nst, mask, rows, ins, dout_p)
+                    reps = max(5, min(60, (512 << 20) // S))
+                    ts = []
+                    for _ in range(reps):
+                        t0 = time.perf_counter()
+                        L.decode_batch(nst, mask, rows, ins, dout_p)
+                        ts.append(time.perf_counter() - t0)
+                    ok = bool(np.array_equal(dout, din))
+                ts.sort()
+                med = ts[len(ts) // 2]
+                print("%d+%d decode %4d MiB: %9.1f us per call, %6.2f GB/s user, ok %s"
+                      % (k, n - k, mib, med * 1e6, S / med / 1e9, ok))
+            finally:
+                for p in bufs:
+                    lib.ec_method_host_free(p)
+
+
+if __name__ == "__main__":
+    main()
