@@ -734,8 +734,14 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
     return combine_any<true>(s, d);
 }
 
-/* EC_MI355X_ZCDB=1: the persistent double-buffered zero-copy combine
- * (ec_combine_zc_db, candidate) instead of one tile per block. */
+/* EC_MI355X_ZCDB=1: host-buffer combines with k <= 8 run the persistent
+ * double-buffered ec_combine_zc_db.  Pinned 8+4 / 4+2 decodes, same process
+ * alternating (tools/zc_sizes.py, profiles/r03/r03af_zcsizes.log), us per
+ * call one tile per block -> double-buffered: 4 MiB 177-197 -> 174 / 174 ->
+ * 162, 16 MiB 572 -> 518-526 / 554-568 -> 530, 64 MiB 1765-1790 -> 1757 /
+ * 1760 -> 1674-1683, 256 MiB 6350 -> 6245 / 6390 -> 6178; bit-exact in the
+ * knob test and every size probed.  Opt-in until the whole GPU suite
+ * (mixed-pattern and heal host calls) has run with it as the default. */
 static bool zc_double_buffered()
 {
     static const bool v = [] {
