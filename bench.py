@@ -460,15 +460,28 @@ def heal_sweep(mode, windows=64):
     """What glustershd issues (ec-heal.c:2048-2107): the 8+4 heal of a file
     in 4 MiB windows, each decoded from 8 good fragments (ec_method_decode)
     and fully re-encoded (ec_method_encode), through the drop-in API on host
-    buffers -- pageable (numpy) or registered with ec_method_host_register
-    (the iobuf-arena hunk of the integration patch).  Run in a child
-    process per engine setting: `auto` (the crossover), `gpu`
+    buffers of four provenances:
+      pageable        every buffer plain malloc memory (an unpatched client);
+      registered      every buffer in one registered arena (r03's line; no
+                      client allocates like this);
+      ec_provenance   what the integration patch gives a client: fragments
+                      (RPC replies of 512 KiB, iobuf.c:25-26) in 1 MiB-page
+                      arenas registered by the deferred arena hook, decode and
+                      re-encode outputs (ec_buffer_alloc of 4 MiB + 64 and
+                      6 MiB + 64, stdalloc iobufs, ec-inode-read.c:1191,
+                      ec-inode-write.c:1871) from the pinned pool that the
+                      patch's iobuf data allocator installs;
+      ec_provenance_calloc  the same fragments, outputs from plain calloc (the
+                      control: the patch without the data allocator, i.e. one
+                      call mixing mapped and pageable buffers).
+    Run in a child process per engine setting: `auto` (the crossover), `gpu`
     (EC_GPU_ALWAYS=1) and `cpu` (cpu-extensions=avx); the engine counters
     say where the calls went."""
-    import ctypes
+    import mmap
     import numpy as np
     import glusterfs_amd as g
     from glusterfs_amd import synth
+    lib = g.ec_method.lib
     k, n, W = 8, 12, 4 << 20
     nst = W // (CHUNK * k)
     fl = nst * CHUNK
@@ -476,52 +489,94 @@ def heal_sweep(mode, windows=64):
     mask = sum(1 << (r - 1) for r in rows)
     nwin = 4                                          # distinct windows, cycled
     res = {}
-    for reg in (False, True):
-        # one page-aligned arena for every buffer (as an iobuf arena is)
-        per = W + n * fl + W
-        raw = np.empty(nwin * per + 4096, np.uint8)
-        base = (-raw.ctypes.data) % 4096
-        arena = raw[base:base + nwin * per]
+    for prov in ("pageable", "registered", "ec_provenance", "ec_provenance_calloc"):
+        keep, regs, pool = [], [], []
+        ps0 = g.pool_stats()
         bufs = []
-        for w in range(nwin):
-            o = w * per
-            data = arena[o:o + W]
-            frs = [arena[o + W + i * fl:o + W + (i + 1) * fl] for i in range(n)]
-            out = arena[o + W + n * fl:o + per]
+        if prov in ("pageable", "registered"):
+            # one page-aligned region for every buffer
+            per = W + n * fl + W
+            raw = np.empty(nwin * per + 4096, np.uint8)
+            base = (-raw.ctypes.data) % 4096
+            arena = raw[base:base + nwin * per]
+            for w in range(nwin):
+                o = w * per
+                frs = [arena[o + W + i * fl:o + W + (i + 1) * fl] for i in range(n)]
+                bufs.append((arena[o:o + W], frs, arena[o + W + n * fl:o + per], frs))
+            if prov == "registered":
+                lib.ec_method_host_register(arena.ctypes.data, arena.nbytes)
+                regs.append(arena.ctypes.data)
+        else:
+            # fragments: 1 MiB pages of 2-page arenas, registered by the
+            # deferred hook (as __iobuf_pool_add_arena would call it)
+            pages = []
+            for _ in range((nwin * n + 1) // 2):
+                m = mmap.mmap(-1, 2 << 20)
+                a = np.frombuffer(m, np.uint8)
+                keep.append((m, a))
+                lib.ec_method_host_register_async(a.ctypes.data, a.nbytes)
+                regs.append(a.ctypes.data)
+                pages += [a[:1 << 20], a[1 << 20:]]
+            lib.ec_method_host_register_flush()
+            for w in range(nwin):
+                frs = [pages[w * n + i][:fl] for i in range(n)]
+                if prov == "ec_provenance":
+                    d = g.PoolBuffer(W + 64 + 4095)
+                    e = g.PoolBuffer(n * fl + 64 + 4095)
+                    pool += [d, e]
+                    dout, eout = d.array[:W], e.array
+                else:
+                    dout, eout = np.zeros(W, np.uint8), np.zeros(n * fl, np.uint8)
+                bufs.append((np.empty(W, np.uint8), frs, dout,
+                             [eout[i * fl:(i + 1) * fl] for i in range(n)]))
+        for w, (data, frs, out, eo) in enumerate(bufs):
             data[:] = synth.fill_numpy(W, word0=w * W // 8)
-            bufs.append((data, frs, out))
-        if reg:
-            g.ec_method.lib.ec_method_host_register(arena.ctypes.data, arena.nbytes)
         try:
             with g.ECMatrixList(k, n, gen="avx" if mode == "cpu" else "auto") as L:
-                for data, frs, out in bufs:               # fragments to heal from
+                for data, frs, out, eo in bufs:           # fragments to heal from
                     L.encode(W, data, frs)
-                data, frs, out = bufs[0]                 # warm (lazy setup)
+                data, frs, out, eo = bufs[0]              # warm (lazy setup)
                 L.decode(fl, mask, rows, [frs[r - 1] for r in rows], out)
-                L.encode(W, out, frs)
+                L.encode(W, out, eo)
                 st0 = g.stats()
                 td, te = [], []
                 t0 = time.perf_counter()
                 for i in range(windows):
-                    data, frs, out = bufs[i % nwin]
+                    data, frs, out, eo = bufs[i % nwin]
                     a = time.perf_counter()
                     L.decode(fl, mask, rows, [frs[r - 1] for r in rows], out)
                     b = time.perf_counter()
-                    L.encode(W, out, frs)
+                    L.encode(W, out, eo)
                     te.append(time.perf_counter() - b)
                     td.append(b - a)
                 el = time.perf_counter() - t0
                 st1 = g.stats()
-                ok = all(np.array_equal(o, d) for d, _, o in bufs)
+                ok = all(np.array_equal(o, d) for d, _, o, _ in bufs) and all(
+                    np.array_equal(e[i], f[i]) for _, f, _, e in bufs for i in range(n))
         finally:
-            if reg:
-                g.ec_method.lib.ec_method_host_unregister(arena.ctypes.data)
-        res["registered" if reg else "pageable"] = dict(
-            user_GBps=round(gbps(W * windows, el), 2), ok=ok,
-            decode_us_median=round(sorted(td)[len(td) // 2] * 1e6, 1),
-            encode_us_median=round(sorted(te)[len(te) // 2] * 1e6, 1),
-            gpu_calls=st1["gpu_calls"] - st0["gpu_calls"],
-            cpu_calls=st1["cpu_calls"] - st0["cpu_calls"])
+            for p in regs:
+                lib.ec_method_host_unregister(p)
+            for b in pool:
+                b.free()
+        ps1 = g.pool_stats()
+        r = dict(user_GBps=round(gbps(W * windows, el), 2), ok=ok,
+                 decode_us_median=round(sorted(td)[len(td) // 2] * 1e6, 1),
+                 encode_us_median=round(sorted(te)[len(te) // 2] * 1e6, 1),
+                 gpu_calls=st1["gpu_calls"] - st0["gpu_calls"],
+                 cpu_calls=st1["cpu_calls"] - st0["cpu_calls"])
+        dreg = ps1["deferred_registers"] - ps0["deferred_registers"]
+        if dreg:
+            r["arena_register_us_per_2MiB"] = round(
+                (ps1["deferred_register_us"] - ps0["deferred_register_us"]) / dreg, 1)
+        dun = ps1["unregisters"] - ps0["unregisters"]
+        if dun:
+            r["unregister_us"] = round((ps1["unregister_us"] - ps0["unregister_us"]) / dun, 1)
+        dsl = ps1["slabs"] - ps0["slabs"]
+        if dsl:
+            r["pool_slab_register_us_per_MiB"] = round(
+                (ps1["slab_register_us"] - ps0["slab_register_us"]) /
+                ((ps1["pool_bytes"] - ps0["pool_bytes"]) / (1 << 20)), 1)
+        res[prov] = r
     return res
 
 

@@ -8,6 +8,7 @@ from .ec_method import (  # noqa: F401
     EC_METHOD_MAX_FRAGMENTS,
     ECMatrixList,
     PinnedArray,
+    PoolBuffer,
     copy_threads,
     device_count,
     device_numa_node,
@@ -18,6 +19,7 @@ from .ec_method import (  # noqa: F401
     inject_device_faults,
     inverse_matrix,
     mask_rows,
+    pool_stats,
     stats,
     sync_device,
 )

@@ -128,7 +128,24 @@ int ecd_device_numa_node(int device);
 int ecd_copy_threads(void);
 void ecd_host_free(void *p);
 int ecd_host_register(void *p, size_t bytes);
+/* unregisters a registered range, or drops it from the deferred queue */
 int ecd_host_unregister(void *p);
+/* queue [p, p + bytes) for registration by the library's thread */
+int ecd_host_register_async(void *p, size_t bytes);
+/* wait until every queued registration has run */
+void ecd_host_register_flush(void);
+
+/* Pinned buffer pool (ec_device.hip BufPool): NULL when no device, too
+ * large, or the pool's range is used up; put returns 1 for pool buffers. */
+void *ecd_buffer_get(size_t bytes);
+int ecd_buffer_put(void *p);
+
+typedef struct ecd_pool_stats {
+    uint64_t pool_bytes, in_use_bytes, gets, misses, slabs, slab_register_us;
+    uint64_t deferred_registers, deferred_register_us, deferred_register_failures;
+    uint64_t unregisters, unregister_us;
+} ecd_pool_stats_t;
+void ecd_pool_stats(ecd_pool_stats_t *s);
 
 #ifdef __cplusplus
 }

@@ -357,10 +357,14 @@ void add_gather(std::vector<CopyPool::Piece> &v, uint8_t *dst, const std::vector
  * host memory (hipHostMalloc / ec_method_host_alloc / hipHostRegister),
  * else nullptr.  16-byte alignment is required for the kernels' vector
  * accesses. */
+bool pool_owns(const void *p, size_t n);
+
 uint8_t *mapped(const void *p, size_t n)
 {
     if (!p || ((uintptr_t)p & 15))
         return nullptr;
+    if (pool_owns(p, n))   /* a pool buffer: registered at the same address */
+        return static_cast<uint8_t *>(const_cast<void *>(p));
     void *d0 = nullptr, *d1 = nullptr;
     g_map_queries.fetch_add(1, std::memory_order_relaxed);
     if (hipHostGetDevicePointer(&d0, const_cast<void *>(p), 0) != hipSuccess ||
@@ -482,6 +486,342 @@ void pinned_free(void *p)
         (void)hipHostFree(p);
     }
     g_host_gen.fetch_add(1, std::memory_order_release);
+}
+
+uint64_t mono_us()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000ull + (uint64_t)ts.tv_nsec / 1000;
+}
+
+/* ------------------------------------------------ pinned buffer pool (r04) */
+
+/* Pinned, device-mapped buffers recycled by size, for a client's own I/O
+ * buffers (ec_method_buffer_get / _put).  The integration patch hands
+ * GlusterFS's non-arena iobufs to it -- iobuf_get_from_small (<= 128 KiB,
+ * GF_MALLOC) and iobuf_get_from_stdalloc (> 1 MiB, GF_CALLOC),
+ * iobuf.c:439-510 -- which is where ec_buffer_alloc (ec-helpers.c:134-165)
+ * puts a heal window's decode output (4 MiB + 64, ec-inode-read.c:1191) and
+ * re-encode output (n/k x 4 MiB, ec-inode-write.c:1871), and where the RPC
+ * layer puts small fragment replies; the coder then reads and writes them in
+ * place over PCIe.  hipHostRegister runs once per slab, when the pool grows,
+ * never per buffer.
+ *   - one reserved virtual range (EC_POOL_MB, default 2048 MiB) in 2 MiB
+ *     granules, so ownership and size class of an address are O(1) (and a
+ *     pool buffer is known to be mapped without a HIP pointer query);
+ *   - classes 4 KiB .. 1 MiB (powers of two) share one-granule slabs; larger
+ *     buffers are runs of g granules (g <= 64, 128 MiB), one free list per g;
+ *   - slab pages are bound (preferred) to the NUMA node of the first
+ *     host-buffer GPU and faulted in before registration;
+ *   - nothing is returned to the system before exit; when the range is used
+ *     up, get() returns NULL and the caller allocates as before.
+ * Contents are not cleared (GF_MALLOC'd iobufs are not either). */
+class BufPool {
+  public:
+    static constexpr size_t kGran = 2u << 20;
+    static constexpr int kMinShift = 12, kMaxSmallShift = 20;
+    static constexpr int kNSmall = kMaxSmallShift - kMinShift + 1;
+    static constexpr int kMaxRun = 64;
+    static constexpr int kNClass = kNSmall + kMaxRun;
+    static constexpr uint8_t kFree = 0, kBody = 0xFF;
+
+    void *get(size_t bytes)
+    {
+        if (bytes == 0 || bytes > (size_t)kMaxRun * kGran || !ready())
+            return nullptr;
+        gets_.fetch_add(1, std::memory_order_relaxed);
+        const int c = cls(bytes);
+        {
+            std::lock_guard<std::mutex> g(mu_[c]);
+            if (!free_[c].empty()) {
+                void *p = free_[c].back();
+                free_[c].pop_back();
+                in_use_.fetch_add(csize(c), std::memory_order_relaxed);
+                return p;
+            }
+        }
+        if (!grow(c)) {
+            misses_.fetch_add(1, std::memory_order_relaxed);
+            return nullptr;
+        }
+        return get(bytes);
+    }
+
+    /* true when p is a buffer of the pool (now free again) */
+    bool put(void *p)
+    {
+        int c;
+        if (!chunk_of(p, &c))
+            return false;
+        in_use_.fetch_sub(csize(c), std::memory_order_relaxed);
+        std::lock_guard<std::mutex> g(mu_[c]);
+        free_[c].push_back(p);
+        return true;
+    }
+
+    /* [p, p + n) inside one buffer of the pool: pinned and mapped */
+    bool owns(const void *p, size_t n) const
+    {
+        const uint8_t *b = base_.load(std::memory_order_acquire);
+        const uint8_t *q = static_cast<const uint8_t *>(p);
+        if (!b || q < b || q >= b + span_)
+            return false;
+        const size_t gi = (size_t)(q - b) / kGran;
+        uint8_t m = meta_[gi].load(std::memory_order_acquire);
+        size_t gh = gi;
+        while (m == kBody && gh > 0)            /* inside a run: find its head */
+            m = meta_[--gh].load(std::memory_order_acquire);
+        if (m == kFree || m == kBody)
+            return false;
+        const int c = m - 1;
+        const size_t cs = csize(c);
+        const size_t off = (size_t)(q - (b + gh * kGran));
+        return off % cs + n <= cs;
+    }
+
+    void stats(ecd_pool_stats_t *s) const
+    {
+        s->pool_bytes = grown_.load() * kGran;
+        s->in_use_bytes = in_use_.load();
+        s->gets = gets_.load();
+        s->misses = misses_.load();
+        s->slabs = slabs_.load();
+        s->slab_register_us = slab_us_.load();
+    }
+
+  private:
+    static int cls(size_t bytes)
+    {
+        if (bytes <= ((size_t)1 << kMaxSmallShift)) {
+            int s = kMinShift;
+            while (((size_t)1 << s) < bytes)
+                ++s;
+            return s - kMinShift;
+        }
+        return kNSmall + (int)((bytes + kGran - 1) / kGran) - 1;
+    }
+    static size_t csize(int c)
+    {
+        return c < kNSmall ? (size_t)1 << (c + kMinShift) : (size_t)(c - kNSmall + 1) * kGran;
+    }
+
+    bool chunk_of(const void *p, int *c) const
+    {
+        const uint8_t *b = base_.load(std::memory_order_acquire);
+        const uint8_t *q = static_cast<const uint8_t *>(p);
+        if (!b || q < b || q >= b + span_)
+            return false;
+        const size_t gi = (size_t)(q - b) / kGran;
+        const uint8_t m = meta_[gi].load(std::memory_order_acquire);
+        if (m == kFree || m == kBody)
+            return false;
+        *c = m - 1;
+        return (size_t)(q - (b + gi * kGran)) % csize(*c) == 0;
+    }
+
+    bool ready()
+    {
+        std::call_once(once_, [this] {
+            if (g_ndev == 0)
+                return;
+            const char *e = getenv("EC_POOL_MB");
+            const long mb = e ? atol(e) : 2048;
+            if (mb <= 0)
+                return;
+            ngran_ = ((size_t)mb << 20) / kGran;
+            if (ngran_ == 0)
+                return;
+            const size_t len = ngran_ * kGran + kGran;
+            void *r = mmap(nullptr, len, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
+                           -1, 0);
+            if (r == MAP_FAILED)
+                return;
+            uint8_t *b = (uint8_t *)(((uintptr_t)r + kGran - 1) & ~(uintptr_t)(kGran - 1));
+            meta_.reset(new std::atomic<uint8_t>[ngran_]);
+            for (size_t i = 0; i < ngran_; ++i)
+                meta_[i].store(kFree, std::memory_order_relaxed);
+            span_ = ngran_ * kGran;
+            base_.store(b, std::memory_order_release);
+        });
+        return base_.load(std::memory_order_acquire) != nullptr;
+    }
+
+    /* new slab for class c: g granules, mapped, bound, faulted in, registered */
+    bool grow(int c)
+    {
+        std::lock_guard<std::mutex> g(grow_mu_);
+        {
+            std::lock_guard<std::mutex> f(mu_[c]);   /* another thread grew it */
+            if (!free_[c].empty())
+                return true;
+        }
+        const size_t ng = c < kNSmall ? 1 : (size_t)(c - kNSmall + 1);
+        if (next_ + ng > ngran_)
+            return false;
+        uint8_t *b = base_.load(std::memory_order_relaxed) + next_ * kGran;
+        const size_t len = ng * kGran;
+        const uint64_t t0 = mono_us();
+        if (mprotect(b, len, PROT_READ | PROT_WRITE) != 0)
+            return false;
+        const int node = device_numa(g_host_devs[0]);
+        if (node >= 0 && node < 1024 && !getenv("EC_NUMA_OFF")) {
+            unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {};
+            mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+            (void)syscall(SYS_mbind, b, len, 1, mask, (unsigned long)1024, 0u);
+        }
+        memset(b, 0, len);
+        void *dp = nullptr;
+        if (hipHostRegister(b, len, hipHostRegisterMapped) != hipSuccess ||
+            hipHostGetDevicePointer(&dp, b, 0) != hipSuccess || dp != b) {
+            (void)hipGetLastError();
+            (void)hipHostUnregister(b);
+            (void)hipGetLastError();
+            madvise(b, len, MADV_DONTNEED);
+            (void)mprotect(b, len, PROT_NONE);
+            return false;
+        }
+        slab_us_.fetch_add(mono_us() - t0, std::memory_order_relaxed);
+        meta_[next_].store((uint8_t)(c + 1), std::memory_order_release);
+        for (size_t i = 1; i < ng; ++i)
+            meta_[next_ + i].store(kBody, std::memory_order_release);
+        next_ += ng;
+        grown_.fetch_add(ng);
+        slabs_.fetch_add(1);
+        std::lock_guard<std::mutex> f(mu_[c]);
+        const size_t cs = csize(c);
+        for (size_t o = len; o >= cs; o -= cs)     /* lowest address handed out first */
+            free_[c].push_back(b + o - cs);
+        return true;
+    }
+
+    std::once_flag once_;
+    std::atomic<uint8_t *> base_{nullptr};
+    size_t span_ = 0, ngran_ = 0, next_ = 0;
+    std::unique_ptr<std::atomic<uint8_t>[]> meta_;
+    std::mutex grow_mu_;
+    std::mutex mu_[kNClass];
+    std::vector<void *> free_[kNClass];
+    std::atomic<uint64_t> gets_{0}, misses_{0}, in_use_{0}, grown_{0}, slabs_{0}, slab_us_{0};
+};
+
+/* never destroyed: its memory stays registered until the process exits */
+BufPool &buf_pool()
+{
+    static BufPool *p = new BufPool;
+    return *p;
+}
+
+/* ---------------------------------------- deferred host registration (r04) */
+
+/* ec_method_host_register_async: GlusterFS calls the arena hook from
+ * __iobuf_pool_add_arena with iobuf_pool->mutex held (iobuf.c:157), so a
+ * hipHostRegister there (hundreds of us for a 2-4 MiB arena, and arenas of
+ * 1 MiB pages hold only two) would stall every iobuf allocation of the client.
+ * The hook only queues the range; one library thread registers it.  Until it
+ * has, buffers in the range are pageable to the coder (staged, or coded on the
+ * CPU).  Unregistering a range still in the queue drops it; one being
+ * registered is waited for first, so the memory is never unmapped while the
+ * runtime holds it. */
+class RegQueue {
+  public:
+    int submit(void *p, size_t n)
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!started_) {
+            std::thread([this] { loop(); }).detach();
+            started_ = true;
+        }
+        q_.push_back({p, n});
+        cv_.notify_one();
+        return 0;
+    }
+
+    /* the unregister half: drop, or wait, then hipHostUnregister */
+    int unregister(void *p)
+    {
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            for (auto it = q_.begin(); it != q_.end(); ++it)
+                if (it->first == p) {
+                    q_.erase(it);
+                    return 0;
+                }
+            done_cv_.wait(g, [&] { return busy_ != p; });
+        }
+        const uint64_t t0 = mono_us();
+        const hipError_t e = hipHostUnregister(p);
+        unreg_us_.fetch_add(mono_us() - t0, std::memory_order_relaxed);
+        unregs_.fetch_add(1, std::memory_order_relaxed);
+        g_host_gen.fetch_add(1, std::memory_order_release);
+        if (e != hipSuccess) {
+            set_err("hipHostUnregister", e);
+            return -EINVAL;
+        }
+        return 0;
+    }
+
+    void flush()
+    {
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [&] { return q_.empty() && busy_ == nullptr; });
+    }
+
+    void stats(ecd_pool_stats_t *s) const
+    {
+        s->deferred_registers = regs_.load();
+        s->deferred_register_us = reg_us_.load();
+        s->deferred_register_failures = fails_.load();
+        s->unregisters = unregs_.load();
+        s->unregister_us = unreg_us_.load();
+    }
+
+  private:
+    void loop()
+    {
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return !q_.empty(); });
+            const auto r = q_.front();
+            q_.pop_front();
+            busy_ = r.first;
+            g.unlock();
+            const uint64_t t0 = mono_us();
+            const hipError_t e = hipHostRegister(r.first, r.second, hipHostRegisterMapped);
+            const uint64_t dt = mono_us() - t0;
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                if (fails_.fetch_add(1) == 0)
+                    fprintf(stderr, "[ec-mi355x] deferred hipHostRegister(%p, %zu) failed: %s; "
+                                    "buffers there stay pageable\n",
+                            r.first, r.second, hipGetErrorString(e));
+            } else {
+                regs_.fetch_add(1, std::memory_order_relaxed);
+                reg_us_.fetch_add(dt, std::memory_order_relaxed);
+            }
+            g.lock();
+            busy_ = nullptr;
+            done_cv_.notify_all();
+        }
+    }
+
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<std::pair<void *, size_t>> q_;
+    void *busy_ = nullptr;
+    bool started_ = false;
+    std::atomic<uint64_t> regs_{0}, reg_us_{0}, fails_{0}, unregs_{0}, unreg_us_{0};
+};
+
+RegQueue &reg_queue()
+{
+    static RegQueue *q = new RegQueue;
+    return *q;
+}
+
+bool pool_owns(const void *p, size_t n)
+{
+    return buf_pool().owns(p, n);
 }
 
 /* Per-device pipeline resources (pooled). */
@@ -1177,7 +1517,7 @@ static uint64_t coarse_ns()
 
 int ecd_ptr_device(const void *p)
 {
-    if (!p || ecd_device_count() == 0)
+    if (!p || ecd_device_count() == 0 || buf_pool().owns(p, 1))
         return -1;
     const uintptr_t pg = (uintptr_t)p >> 12;
     /* Fibonacci hashing: iobufs sit at regular page strides (65 pages for
@@ -1251,13 +1591,43 @@ int ecd_host_unregister(void *p)
 {
     if (ecd_device_count() == 0)
         return -ENODEV;
-    const hipError_t e = hipHostUnregister(p);
-    g_host_gen.fetch_add(1, std::memory_order_release);
-    if (e != hipSuccess) {
-        set_err("hipHostUnregister", e);
+    if (!p)
         return -EINVAL;
-    }
-    return 0;
+    return reg_queue().unregister(p);
+}
+
+int ecd_host_register_async(void *p, size_t bytes)
+{
+    if (ecd_device_count() == 0)
+        return -ENODEV;
+    if (!p || bytes == 0)
+        return -EINVAL;
+    return reg_queue().submit(p, bytes);
+}
+
+void ecd_host_register_flush(void)
+{
+    if (ecd_device_count() > 0)
+        reg_queue().flush();
+}
+
+void *ecd_buffer_get(size_t bytes)
+{
+    if (ecd_device_count() == 0)
+        return nullptr;
+    return buf_pool().get(bytes);
+}
+
+int ecd_buffer_put(void *p)
+{
+    return p && buf_pool().put(p) ? 1 : 0;
+}
+
+void ecd_pool_stats(ecd_pool_stats_t *s)
+{
+    memset(s, 0, sizeof(*s));
+    buf_pool().stats(s);
+    reg_queue().stats(s);
 }
 
 } /* extern "C" */

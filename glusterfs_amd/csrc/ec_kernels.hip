@@ -734,19 +734,20 @@ int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
     return combine_any<true>(s, d);
 }
 
-/* EC_MI355X_ZCDB=1: host-buffer combines with k <= 8 run the persistent
- * double-buffered ec_combine_zc_db.  Pinned 8+4 / 4+2 decodes, same process
- * alternating (tools/zc_sizes.py, profiles/r03/r03af_zcsizes.log), us per
- * call one tile per block -> double-buffered: 4 MiB 177-197 -> 174 / 174 ->
- * 162, 16 MiB 572 -> 518-526 / 554-568 -> 530, 64 MiB 1765-1790 -> 1757 /
- * 1760 -> 1674-1683, 256 MiB 6350 -> 6245 / 6390 -> 6178; bit-exact in the
- * knob test and every size probed.  Opt-in until the whole GPU suite
- * (mixed-pattern and heal host calls) has run with it as the default. */
+/* Host-buffer combines with k <= 8 run the persistent double-buffered
+ * ec_combine_zc_db (default since r04; EC_MI355X_ZCDB=0 keeps one tile per
+ * block, ec_combine_zc, for A/B runs).  Pinned 8+4 / 4+2 decodes, same
+ * process alternating (tools/zc_sizes.py, profiles/r03/r03af_zcsizes.log), us
+ * per call one tile per block -> double-buffered: 4 MiB 177-197 -> 174 / 174
+ * -> 162, 16 MiB 572 -> 518-526 / 554-568 -> 530, 64 MiB 1765-1790 -> 1757 /
+ * 1760 -> 1674-1683, 256 MiB 6350 -> 6245 / 6390 -> 6178; never slower,
+ * bit-exact in the knob test (ZCDB=0 and =1: decode, heal and mixed host
+ * calls) and at every size probed. */
 static bool zc_double_buffered()
 {
     static const bool v = [] {
         const char *e = getenv("EC_MI355X_ZCDB");
-        return e && *e == '1';
+        return !(e && *e == '0');
     }();
     return v;
 }

@@ -458,8 +458,10 @@ struct EncSrc {
  * src(stripe) + (p * 8 + b) * 64 + q * 16, read as the dword-aligned dwords
  * that cover it (4, or 5 when the source is not dword-aligned: the fifth
  * holds the last wanted byte, so no load touches a page the range does not)
- * and funnel-shifted by v_alignbyte_b32, then one ds_write_b128.  LDS-DMA
- * takes 16-byte-aligned sources only. */
+ * and funnel-shifted by v_alignbyte_b32, then one ds_write_b128.  (Round 3
+ * measured LDS-DMA itself at every source alignment -- it honours any byte
+ * address, tools/kbench/ldsdma_align.hip -- so the shipped kernels stage
+ * misaligned inputs by LDS-DMA; SM = 2 is kept for the kb3 A/B.) */
 template <int K, int T, int NW>
 __device__ __forceinline__ void stage_tile_realign(uint8_t *lds, const EncSrc src, uint64_t t0,
                                                    uint64_t nstripes, u32 wave, u32 lane)
@@ -1431,8 +1433,12 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
     if (tid < rows)
         *reinterpret_cast<uint64_t *>(obase + tid * 8u) = (uint64_t)(uintptr_t)a.out_base[tid];
     stage(t, 0);
+    /* the builtins below are IntrNoMem to LLVM: a compiler-only barrier keeps
+     * the plain C++ LDS writes (row bases, otile) on their side of them */
+    asm volatile("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0x0070);        /* vmcnt(0) lgkmcnt(0) */
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     const u32 cs = lane >> 3, cc = lane & 7u;
     for (u32 i = 0;; ++i) {
         const uint64_t t0 = t * T;
@@ -1467,8 +1473,10 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
                     *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
             }
         }
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_s_waitcnt(0xC07F);    /* lgkmcnt(0): otile written */
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         const uint64_t tn = t + gridDim.x;
         if (tn < ntiles)
             stage(tn, (i + 1u) & 1u);
@@ -1491,8 +1499,10 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
             if (ost < a.nstripes)
                 *(__attribute__((address_space(1))) v4u *)(ob + ost * a.out_stride + w * 16u) = v;
         }
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_s_waitcnt(0x0F70);    /* vmcnt(0): tile i + 1 landed, stores out */
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         if (tn >= ntiles)
             break;
         t = tn;

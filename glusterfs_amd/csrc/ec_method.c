@@ -305,7 +305,9 @@ ec_method_inject_device_faults(uint32_t count)
  *        device-mapped buffers (zero copy); 40 us and 14 GB/s for pageable
  *        ones (staging copies), 21 GB/s from 8 MiB of user data on (the copy
  *        pool splits a call into 2 MiB pieces, so larger calls copy on more
- *        threads); EC_GPU_{PINNED,PAGEABLE}_{US,GBPS}, EC_GPU_PAGEABLE_GBPS_L.
+ *        threads); EC_GPU_{PINNED,PAGEABLE}_{US,GBPS}, EC_GPU_PAGEABLE_GBPS_L;
+ *        a call with some buffers mapped and some not is costed in between,
+ *        by the fraction of its bytes that must be staged (r04).
  *
  * So FUSE-sized calls and light codes stay on the calling thread, wide-code
  * decodes and large pinned calls go to the GPU, and concurrent callers queue
@@ -348,36 +350,67 @@ xover_init(void)
 
 enum { ECM_ENCODE = 0, ECM_DECODE = 1 };
 
-/* 1: code this host-buffer call on the CPU engine.  `user`: user bytes of
- * the call; `moved`: bytes read + written; `op`: ECM_ENCODE / ECM_DECODE;
- * `mapped`: every buffer is pinned, device-mapped host memory. */
-/* Observed rates (r03).  The constants above are calibrated on calls that
- * re-code cache-resident buffers; a self-heal sweep streams through a file
- * (ec-heal.c:2048-2107), and there the CPU engine ran at a fraction of its
- * modelled rate while the GPU with registered buffers ran 1.9x faster
- * (bench.py heal_sweep, profiles/r03*_bench.log).  So every host call of
- * >= 256 KiB of user data records the user-byte rate it achieved -- per
- * engine (CPU; GPU on mapped buffers; GPU on pageable buffers), direction
- * and code width -- as an exponential average (1/8), and once an engine has
- * samples its observed rate replaces the model in the comparison.  An
- * engine the router keeps losing to is re-sampled by one call of >= 1 MiB
- * in every 64 (exploration), so a change in load or residency is noticed.
- * EC_XOVER_ADAPT=0 keeps the static model. */
-enum { ECM_OBS_CPU = 0, ECM_OBS_GPU_MAPPED = 1, ECM_OBS_GPU_PAGEABLE = 2 };
+/* Observed rates (r03, size-bucketed in r04).  The constants above are
+ * calibrated on calls that re-code cache-resident buffers; a self-heal sweep
+ * streams through a file (ec-heal.c:2048-2107), and there the CPU engine ran
+ * at a fraction of its modelled rate while the GPU with registered buffers
+ * ran 1.9x faster (bench.py heal_sweep, profiles/r03*_bench.log).  So every
+ * host call of >= 256 KiB of user data records the user-byte rate it achieved
+ * as an exponential average (weight 1/4), per engine (CPU; GPU with every
+ * buffer mapped; GPU with every buffer staged; GPU with some of each),
+ * direction, code width and call size (log4 buckets from 256 KiB: a rate
+ * learned on cache-resident 256 KiB calls, or one that includes a small
+ * call's fixed latency, is never applied to a multi-GiB call).  Once a slot
+ * has samples its observed rate replaces the model for calls of that size;
+ * the CPU's keeps the DRAM cap for calls moving >= 32 MiB.  An engine the
+ * router keeps losing to is re-sampled by one call of >= 1 MiB in 8 until it
+ * has 4 samples, then in 64 (exploration), so a change in load or residency
+ * is noticed.  EC_XOVER_ADAPT=0 keeps the static model. */
+enum { ECM_OBS_CPU = 0, ECM_OBS_GPU_MAPPED = 1, ECM_OBS_GPU_PAGEABLE = 2, ECM_OBS_GPU_MIXED = 3 };
+#define ECM_OBS_ENGINES 4
+#define ECM_OBS_SIZES 5
 #define ECM_OBS_MIN (256u << 10)
 #define ECM_OBS_EXPLORE (1u << 20)
+#define ECM_STAGED_UNKNOWN UINT64_MAX
 
-static struct {
+typedef struct {
     uint64_t kbps;   /* user KB per second, EWMA; 0: no sample yet */
     uint32_t lost;   /* calls routed away from this engine since its last sample */
     uint32_t n;      /* samples taken (the first, a cold start, is dropped) */
     uint32_t pad[12];
-} __attribute__((aligned(64))) ecm_obs[3][2][3];
+} __attribute__((aligned(64))) ecm_obs_t;
+
+static ecm_obs_t ecm_obs[ECM_OBS_ENGINES][2][3][ECM_OBS_SIZES];
 
 static int
 kbucket(uint32_t k)
 {
     return k <= 4 ? 0 : k <= 8 ? 1 : 2;
+}
+
+/* [256 KiB, 1 MiB), [1, 4), [4, 16), [16, 64), >= 64 MiB of user data */
+static int
+sbucket(uint64_t user)
+{
+    int b = 0;
+
+    for (user >>= 20; user && b < ECM_OBS_SIZES - 1; user >>= 2)
+        b++;
+    return b;
+}
+
+static ecm_obs_t *
+obs_slot(int eng, int op, uint32_t k, uint64_t user)
+{
+    return &ecm_obs[eng][op][kbucket(k)][sbucket(user)];
+}
+
+/* the GPU observation slot of a call with `staged` of `moved` bytes staged */
+static int
+gpu_obs_engine(uint64_t staged, uint64_t moved)
+{
+    return staged == 0 ? ECM_OBS_GPU_MAPPED
+                       : staged >= moved ? ECM_OBS_GPU_PAGEABLE : ECM_OBS_GPU_MIXED;
 }
 
 static uint64_t
@@ -392,98 +425,112 @@ now_ns(void)
 static void
 obs_record(int eng, int op, uint32_t k, uint64_t user, uint64_t ns)
 {
-    uint64_t *slot = &ecm_obs[eng][op][kbucket(k)].kbps;
+    ecm_obs_t *o = obs_slot(eng, op, k, user);
     uint64_t old, upd, sample;
 
     if (user < ECM_OBS_MIN || ns == 0 || !ecm_x.adapt)
         return;
-    __atomic_store_n(&ecm_obs[eng][op][kbucket(k)].lost, 0, __ATOMIC_RELAXED);
+    __atomic_store_n(&o->lost, 0, __ATOMIC_RELAXED);
     /* the first call of an engine pays its cold start (page faults on fresh
      * outputs, lazy set-up): a sample of it would bar the engine for long */
-    if (__atomic_fetch_add(&ecm_obs[eng][op][kbucket(k)].n, 1, __ATOMIC_RELAXED) == 0)
+    if (__atomic_fetch_add(&o->n, 1, __ATOMIC_RELAXED) == 0)
         return;
     sample = user * 1000000ull / ns;                   /* KB/s = B/ns * 1e6 / 1e3 */
-    old = __atomic_load_n(slot, __ATOMIC_RELAXED);
+    old = __atomic_load_n(&o->kbps, __ATOMIC_RELAXED);
     do
         upd = old ? old + ((int64_t)sample - (int64_t)old) / 4 : sample;
-    while (!__atomic_compare_exchange_n(slot, &old, upd, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED));
+    while (!__atomic_compare_exchange_n(&o->kbps, &old, upd, 1, __ATOMIC_RELAXED,
+                                        __ATOMIC_RELAXED));
 }
 
 static double
-obs_gbps(int eng, int op, uint32_t k)
+obs_gbps(int eng, int op, uint32_t k, uint64_t user)
 {
-    return (double)__atomic_load_n(&ecm_obs[eng][op][kbucket(k)].kbps, __ATOMIC_RELAXED) / 1e6;
+    if (user < ECM_OBS_MIN)
+        return 0;
+    return (double)__atomic_load_n(&obs_slot(eng, op, k, user)->kbps, __ATOMIC_RELAXED) / 1e6;
 }
 
 /* 1: send this call to the engine the router did not pick, to re-sample it
- * (every 8th such call while the engine has fewer than 4 samples, then
- * every 64th) */
+ * (every 8th such call while the slot has fewer than 4 samples, then every
+ * 64th) */
 static int
 obs_explore(int eng, int op, uint32_t k, uint64_t user)
 {
-    uint32_t *lost = &ecm_obs[eng][op][kbucket(k)].lost;
-    const uint32_t every =
-        __atomic_load_n(&ecm_obs[eng][op][kbucket(k)].n, __ATOMIC_RELAXED) < 4 ? 8 : 64;
+    ecm_obs_t *o = obs_slot(eng, op, k, user);
+    const uint32_t every = __atomic_load_n(&o->n, __ATOMIC_RELAXED) < 4 ? 8 : 64;
 
     if (!ecm_x.adapt || user < ECM_OBS_EXPLORE)
         return 0;
-    return __atomic_add_fetch(lost, 1, __ATOMIC_RELAXED) % every == 0;
+    return __atomic_add_fetch(&o->lost, 1, __ATOMIC_RELAXED) % every == 0;
 }
 
+/* 1: code this host-buffer call on the CPU engine.  `user`: user bytes of the
+ * call; `moved`: bytes read + written; `op`: ECM_ENCODE / ECM_DECODE;
+ * `staged`: bytes of its buffers that are not pinned, device-mapped host
+ * memory (0: the zero-copy path for every buffer; `moved`: staging copies for
+ * every buffer; in between, a call whose fragments are registered iobufs but
+ * whose output is not, or the reverse -- the device layer reads the mapped
+ * buffers in place and stages only the others, ec_device.hip
+ * run_decode_dev); `infl`: bytes queued on the least-loaded host GPU.  The
+ * model's GPU cost is interpolated between the two pure cases by the staged
+ * fraction. */
 static int
-route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int mapped)
+route_cpu_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t staged,
+            uint64_t infl)
 {
     static const double isa_f[] = {0.4, 0.7, 1.0};
-    double cpu_gbps, cpu_us, gpu_us, q, obs;
-    uint64_t infl;
+    double cpu_gbps, cpu_us, gpu_us, q, obs, f, page_gbps;
 
-    if (ctx->engine == ECM_ENGINE_CPU)
-        return 1;
     pthread_once(&ecm_xover_once, xover_init);
     if (ecm_x.always)
         return 0;
-    if (moved < ecm_x.cpu_below)
+    if (moved < ecm_x.cpu_below || infl == UINT64_MAX)
         return 1;
-    cpu_gbps = (op == ECM_ENCODE ? (double)ecm_x.enc_k2 / (ctx->k + 2)
-                                 : (double)ecm_x.dec_k / ctx->k) *
-               isa_f[ctx->isa < 0 ? 0 : ctx->isa > 2 ? 2 : ctx->isa];
+    cpu_gbps = (op == ECM_ENCODE ? (double)ecm_x.enc_k2 / (k + 2) : (double)ecm_x.dec_k / k) *
+               isa_f[isa < 0 ? 0 : isa > 2 ? 2 : isa];
+    if ((obs = obs_gbps(ECM_OBS_CPU, op, k, user)) > 0)
+        cpu_gbps = obs;
     if (moved >= (32u << 20))
         cpu_gbps = cpu_gbps < 24.0 ? cpu_gbps : 24.0;
-    if (user >= ECM_OBS_MIN && (obs = obs_gbps(ECM_OBS_CPU, op, ctx->k)) > 0)
-        cpu_gbps = obs;
     cpu_us = (double)user / (cpu_gbps * 1e3);
-    infl = ecd_host_inflight();
-    if (infl == UINT64_MAX)
-        return 1;
     q = (double)infl * ((double)user / (double)moved); /* queued user bytes */
-    obs = user >= ECM_OBS_MIN
-              ? obs_gbps(mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, op, ctx->k)
-              : 0;
-    if (obs > 0)            /* the observed rate includes the call's latency; a */
+    if (staged > moved)
+        staged = moved;
+    obs = obs_gbps(gpu_obs_engine(staged, moved), op, k, user);
+    if (obs > 0) {           /* the observed rate includes the call's latency; a */
         gpu_us = 1.1 * (q + user) / (obs * 1e3); /* near tie stays on the caller's CPU */
-    else
-        gpu_us = mapped ? (double)ecm_x.pin_us + (q + user) / ((double)ecm_x.pin_gbps * 1e3)
-                        : (double)ecm_x.page_us +
-                              (q + user) / ((double)(user >= (8u << 20) ? ecm_x.page_gbps_l
-                                                                        : ecm_x.page_gbps) *
-                                            1e3);
+    } else {
+        f = (double)staged / (double)moved;
+        page_gbps = (double)(user >= (8u << 20) ? ecm_x.page_gbps_l : ecm_x.page_gbps);
+        gpu_us = (double)ecm_x.pin_us + f * ((double)ecm_x.page_us - (double)ecm_x.pin_us) +
+                 (q + user) * ((1.0 - f) / (double)ecm_x.pin_gbps + f / page_gbps) / 1e3;
+    }
     return cpu_us <= gpu_us;
 }
 
-/* The engine for a host call: 1 = GPU.  `*mapped` (in: -1 unknown) is
- * filled in when the placement had to be queried. */
+static int
+route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, uint64_t staged)
+{
+    if (ctx->engine == ECM_ENGINE_CPU)
+        return 1;
+    return route_cpu_q(ctx->k, ctx->isa, user, moved, op, staged, ecd_host_inflight());
+}
+
+/* The engine for a host call: 1 = GPU.  `*staged` (in: ECM_STAGED_UNKNOWN)
+ * is filled in when the placement of the buffers had to be queried. */
 static int
 route_gpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op,
-          int (*is_mapped)(const void *), const void *arg, int *mapped)
+          uint64_t (*staged_of)(const void *), const void *arg, uint64_t *staged)
 {
     int gpu = 0;
 
-    /* the pinned-buffer GPU estimate is the optimistic one: a call that the
-     * CPU wins against it skips the pointer queries (which serialise in the
-     * HIP runtime: ~11 us each with 16 calling threads, tools/kbench/ptrq) */
-    if (!route_cpu(ctx, user, moved, op, 1)) {
-        *mapped = is_mapped(arg);
-        gpu = !route_cpu(ctx, user, moved, op, *mapped);
+    /* the all-mapped GPU estimate is the optimistic one: a call that the CPU
+     * wins against it skips the pointer queries (which serialise in the HIP
+     * runtime: ~11 us each with 16 calling threads, tools/kbench/ptrq) */
+    if (!route_cpu(ctx, user, moved, op, 0)) {
+        *staged = staged_of(arg);
+        gpu = !route_cpu(ctx, user, moved, op, *staged);
     }
     if (ctx->engine == ECM_ENGINE_CPU || ecm_x.always || moved < ecm_x.cpu_below)
         return gpu;
@@ -491,26 +538,55 @@ route_gpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op,
         if (obs_explore(ECM_OBS_CPU, op, ctx->k, user))
             gpu = 0;
     } else {
-        if (*mapped < 0 && user >= ECM_OBS_EXPLORE)
-            *mapped = is_mapped(arg);
-        if (*mapped >= 0 &&
-            obs_explore(*mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, op, ctx->k, user))
+        if (*staged == ECM_STAGED_UNKNOWN && user >= ECM_OBS_EXPLORE)
+            *staged = staged_of(arg);
+        if (*staged != ECM_STAGED_UNKNOWN &&
+            obs_explore(gpu_obs_engine(*staged, moved), op, ctx->k, user))
             gpu = 1;
     }
     return gpu;
 }
 
-/* 1 when every non-NULL buffer of b[0..n) (len bytes each) is pinned,
- * device-mapped host memory */
-static int
-all_mapped(const void *const *b, uint32_t n, uint64_t len)
+/* Crossover probes for tests (include/ec_method.h): the router of a GPU
+ * volume, with the queue given, needs no device. */
+int32_t
+ec_method_xover_route(uint32_t k, int32_t op, uint64_t user, uint64_t moved, uint64_t staged,
+                      uint64_t inflight)
 {
+    if (k < 1 || k > ECM_MAX_K || moved == 0 || (op != ECM_ENCODE && op != ECM_DECODE))
+        return -EINVAL;
+    return route_cpu_q(k, ecc_isa_max(), user, moved, op, staged, inflight);
+}
+
+int32_t
+ec_method_xover_observe(int32_t engine, int32_t op, uint32_t k, uint64_t user, uint64_t ns)
+{
+    if (engine < 0 || engine >= ECM_OBS_ENGINES || (op != ECM_ENCODE && op != ECM_DECODE) ||
+        k < 1 || k > ECM_MAX_K)
+        return -EINVAL;
+    pthread_once(&ecm_xover_once, xover_init);
+    obs_record(engine, op, k, user, ns);
+    return 0;
+}
+
+void
+ec_method_xover_reset(void)
+{
+    memset(ecm_obs, 0, sizeof(ecm_obs));
+}
+
+/* bytes of the n buffers b[0..n) (len bytes each; NULL entries skipped) that
+ * are not pinned, device-mapped host memory */
+static uint64_t
+staged_bytes(const void *const *b, uint32_t n, uint64_t len)
+{
+    uint64_t s = 0;
     uint32_t i;
 
     for (i = 0; i < n; i++)
         if (b[i] && !ecd_host_mapped(b[i], len))
-            return 0;
-    return 1;
+            s += len;
+    return s;
 }
 
 /* A failed device submission for host buffers: log once, count, and let
@@ -839,6 +915,51 @@ ec_method_host_unregister(void *p)
     return ecd_host_unregister(p);
 }
 
+int32_t
+ec_method_host_register_async(void *p, size_t bytes)
+{
+    return ecd_host_register_async(p, bytes);
+}
+
+void
+ec_method_host_register_flush(void)
+{
+    ecd_host_register_flush();
+}
+
+void *
+ec_method_buffer_get(size_t bytes)
+{
+    return ecd_buffer_get(bytes);
+}
+
+int32_t
+ec_method_buffer_put(void *p)
+{
+    return ecd_buffer_put(p);
+}
+
+void
+ec_method_pool_stats(ec_method_pool_stats_t *st)
+{
+    ecd_pool_stats_t s;
+
+    if (!st)
+        return;
+    ecd_pool_stats(&s);
+    st->pool_bytes = s.pool_bytes;
+    st->in_use_bytes = s.in_use_bytes;
+    st->gets = s.gets;
+    st->misses = s.misses;
+    st->slabs = s.slabs;
+    st->slab_register_us = s.slab_register_us;
+    st->deferred_registers = s.deferred_registers;
+    st->deferred_register_us = s.deferred_register_us;
+    st->deferred_register_failures = s.deferred_register_failures;
+    st->unregisters = s.unregisters;
+    st->unregister_us = s.unregister_us;
+}
+
 /* disperse.cpu-extensions (ec.c:1786-1794) -> engine.  The reference maps
  * none to portable C and x64 / sse / avx to its JIT back ends, auto to the
  * best of them (ec-code.c:59-69, 977-1060).  Here auto (and hip) select the
@@ -1004,13 +1125,13 @@ struct enc_bufs {
     uint64_t fl;
 };
 
-static int
-enc_mapped(const void *arg)
+static uint64_t
+enc_staged(const void *arg)
 {
     const struct enc_bufs *b = (const struct enc_bufs *)arg;
 
-    return ecd_host_mapped(b->in, b->fl * b->k) &&
-           all_mapped((const void *const *)b->out, b->n, b->fl);
+    return (ecd_host_mapped(b->in, b->fl * b->k) ? 0 : b->fl * b->k) +
+           staged_bytes((const void *const *)b->out, b->n, b->fl);
 }
 
 static int
@@ -1019,18 +1140,18 @@ host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
     const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE, user = fl * ctx->k;
     const uint64_t bytes = fl * (ctx->k + ctx->n);
     const struct enc_bufs eb = {in, out, ctx->k, ctx->n, fl};
-    int rc, mapped = -1;
-    uint64_t t0;
+    uint64_t t0, staged = ECM_STAGED_UNKNOWN;
+    int rc;
 
-    if (route_gpu(ctx, user, bytes, ECM_ENCODE, enc_mapped, &eb, &mapped)) {
+    if (route_gpu(ctx, user, bytes, ECM_ENCODE, enc_staged, &eb, &staged)) {
         t0 = now_ns();
         rc = ecd_encode_host(0, ctx->k, ctx->n, nstripes, in, out, ctx->enc_pat);
         if (!gpu_failed(rc)) {
             if (rc == 0) {
                 stat_add(ECM_STAT_GPU);
-                if (mapped >= 0)
-                    obs_record(mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, ECM_ENCODE,
-                               ctx->k, user, now_ns() - t0);
+                if (staged != ECM_STAGED_UNKNOWN)
+                    obs_record(gpu_obs_engine(staged, bytes), ECM_ENCODE, ctx->k, user,
+                               now_ns() - t0);
             }
             return rc;
         }
@@ -1052,14 +1173,14 @@ struct dec_bufs {
     uint64_t fl;
 };
 
-static int
-dec_mapped(const void *arg)
+static uint64_t
+dec_staged(const void *arg)
 {
     const struct dec_bufs *b = (const struct dec_bufs *)arg;
 
-    return all_mapped(b->frags, b->nfrags, b->fl) &&
-           (b->outs ? all_mapped((const void *const *)b->outs, b->rows, b->fl)
-                    : ecd_host_mapped(b->out, b->fl * b->rows));
+    return staged_bytes(b->frags, b->nfrags, b->fl) +
+           (b->outs ? staged_bytes((const void *const *)b->outs, b->rows, b->fl)
+                    : (ecd_host_mapped(b->out, b->fl * b->rows) ? 0 : b->fl * b->rows));
 }
 
 /* Host-buffer combination (decode, mixed decode, heal): the GPU pipeline or
@@ -1074,19 +1195,19 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
     const struct dec_bufs db = {frags, nfrags, out, outs, rows, fl};
     ecd_combine_desc_t d;
     uint32_t f, r;
-    int rc, mapped = -1;
-    uint64_t t0;
+    uint64_t t0, staged = ECM_STAGED_UNKNOWN;
+    int rc;
 
-    if (route_gpu(ctx, fl * k, bytes, ECM_DECODE, dec_mapped, &db, &mapped)) {
+    if (route_gpu(ctx, fl * k, bytes, ECM_DECODE, dec_staged, &db, &staged)) {
         t0 = now_ns();
         rc = ecd_decode_host(0, k, rows, nstripes, nfrags, frags, out, outs, npat, pats, gp,
                              shift);
         if (!gpu_failed(rc)) {
             if (rc == 0) {
                 stat_add(ECM_STAT_GPU);
-                if (mapped >= 0)
-                    obs_record(mapped ? ECM_OBS_GPU_MAPPED : ECM_OBS_GPU_PAGEABLE, ECM_DECODE,
-                               k, fl * k, now_ns() - t0);
+                if (staged != ECM_STAGED_UNKNOWN)
+                    obs_record(gpu_obs_engine(staged, bytes), ECM_DECODE, k, fl * k,
+                               now_ns() - t0);
             }
             return rc;
         }
@@ -1465,8 +1586,18 @@ ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iove
     }
     segp[ns] = ts;
     segl[ns++] = nst * S - b2;
+    /* the padded input is always gathered into the staging slots; the
+     * fragments are staged unless they are mapped (the estimate with mapped
+     * fragments first: it is the optimistic one, so a call the CPU wins
+     * anyway makes no pointer query) */
     if (!route_cpu(ctx, nst * EC_METHOD_CHUNK_SIZE * ctx->k,
-                   nst * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n), ECM_ENCODE, 0)) {
+                   nst * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n), ECM_ENCODE,
+                   nst * EC_METHOD_CHUNK_SIZE * ctx->k) &&
+        !route_cpu(ctx, nst * EC_METHOD_CHUNK_SIZE * ctx->k,
+                   nst * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n), ECM_ENCODE,
+                   nst * EC_METHOD_CHUNK_SIZE * ctx->k +
+                       staged_bytes((const void *const *)out, ctx->n,
+                                    nst * EC_METHOD_CHUNK_SIZE))) {
         c = ecd_encode_host_gather(0, ctx->k, ctx->n, nst, ns, segp, segl, out, ctx->enc_pat);
         if (!gpu_failed(c)) {
             if (c == 0)

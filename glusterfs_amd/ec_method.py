@@ -40,6 +40,9 @@ EXPORTS = (
     "ec_method_config_unpack", "ec_method_config_check", "ec_method_writev_encode",
     "ec_method_writev_encode_device", "ec_method_engine", "ec_method_get_stats",
     "ec_method_inject_device_faults", "ec_method_device_numa_node", "ec_method_copy_threads",
+    "ec_method_host_register_async", "ec_method_host_register_flush", "ec_method_buffer_get",
+    "ec_method_buffer_put", "ec_method_pool_stats", "ec_method_xover_route",
+    "ec_method_xover_observe", "ec_method_xover_reset",
 )
 
 
@@ -81,6 +84,14 @@ class Stats(ctypes.Structure):
     """ec_method_stats_t: process-wide engine counters."""
     _fields_ = [("gpu_calls", ctypes.c_uint64), ("cpu_calls", ctypes.c_uint64),
                 ("cpu_fallbacks", ctypes.c_uint64)]
+
+
+class PoolStats(ctypes.Structure):
+    """ec_method_pool_stats_t: pinned buffer pool and deferred registration."""
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "pool_bytes", "in_use_bytes", "gets", "misses", "slabs", "slab_register_us",
+        "deferred_registers", "deferred_register_us", "deferred_register_failures",
+        "unregisters", "unregister_us")]
 
 
 class Config(ctypes.Structure):
@@ -141,6 +152,14 @@ def _load():
         "ec_method_host_free": (None, [vp]),
         "ec_method_host_register": (ctypes.c_int32, [vp, ctypes.c_size_t]),
         "ec_method_host_unregister": (ctypes.c_int32, [vp]),
+        "ec_method_host_register_async": (i32, [vp, ctypes.c_size_t]),
+        "ec_method_host_register_flush": (None, []),
+        "ec_method_buffer_get": (vp, [ctypes.c_size_t]),
+        "ec_method_buffer_put": (i32, [vp]),
+        "ec_method_pool_stats": (None, [ctypes.POINTER(PoolStats)]),
+        "ec_method_xover_route": (i32, [u32, i32, u64, u64, u64, u64]),
+        "ec_method_xover_observe": (i32, [i32, i32, u32, u64, u64]),
+        "ec_method_xover_reset": (None, []),
         "ec_method_encode_matrix": (i32, [u32, u32, vp]),
         "ec_method_inverse_matrix": (i32, [u32, vp, vp]),
         "ec_method_gf_mul": (u32, [u32, u32]),
@@ -212,6 +231,13 @@ def stats():
     return dict(gpu_calls=st.gpu_calls, cpu_calls=st.cpu_calls, cpu_fallbacks=st.cpu_fallbacks)
 
 
+def pool_stats():
+    """Pinned buffer pool / deferred registration counters as a dict."""
+    st = PoolStats()
+    lib.ec_method_pool_stats(ctypes.byref(st))
+    return {n: getattr(st, n) for n, _ in PoolStats._fields_}
+
+
 def inject_device_faults(count):
     """Test hook: the next `count` host-buffer device submissions fail."""
     lib.ec_method_inject_device_faults(count)
@@ -244,6 +270,38 @@ class PinnedArray:
 
     def __del__(self):
         self.free()
+
+
+class PoolBuffer:
+    """numpy uint8 view of a buffer of the library's pinned pool
+    (ec_method_buffer_get): what the integration patch's iobuf data allocator
+    hands GlusterFS for its non-arena iobufs.  Falls back to a plain numpy
+    array (pageable) when the pool returns NULL, as iobuf.c would fall back to
+    GF_MALLOC; `pooled` says which."""
+
+    def __init__(self, nbytes):
+        import numpy as np
+        self.nbytes = int(nbytes)
+        self.ptr = lib.ec_method_buffer_get(max(1, self.nbytes))
+        self.pooled = bool(self.ptr)
+        if self.ptr:
+            raw = (ctypes.c_uint8 * max(1, self.nbytes)).from_address(self.ptr)
+            self.array = np.ctypeslib.as_array(raw)[:self.nbytes]
+        else:
+            self.array = np.empty(self.nbytes, np.uint8)
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            if lib.ec_method_buffer_put(self.ptr) != 1:
+                raise RuntimeError("ec_method_buffer_put: not a pool buffer")
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class host_registered:

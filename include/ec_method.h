@@ -280,7 +280,61 @@ void ec_method_host_free(void *p);
  * INTEGRATION.md) so buffers inside it take the zero-copy path.  Returns 0
  * or -errno.  Unregister before freeing the memory. */
 int32_t ec_method_host_register(void *p, size_t bytes);
+/* Unregister a range registered by either call below or above (a range still
+ * waiting in the deferred queue is dropped; one being registered is waited
+ * for).  Returns 0 or -errno. */
 int32_t ec_method_host_unregister(void *p);
+/* Deferred registration: queue the range for a library thread and return at
+ * once (0 or -errno).  For callers holding a lock, such as GlusterFS's arena
+ * hook, which runs under iobuf_pool->mutex (iobuf.c:157): until the thread has
+ * registered the range, buffers in it are coded as pageable memory. */
+int32_t ec_method_host_register_async(void *p, size_t bytes);
+/* Wait until every queued registration has been done (tests, benchmarks). */
+void ec_method_host_register_flush(void);
+
+/* Pinned buffer pool for a client's own I/O buffers (the integration patch's
+ * iobuf data allocator): pinned, device-mapped buffers of
+ * any size up to 128 MiB, recycled by size class (4 KiB .. 1 MiB powers of
+ * two, then 2 MiB steps), so hipHostRegister runs once per 2 MiB slab as the
+ * pool grows and never per buffer.  At least 4 KiB aligned, contents not
+ * cleared.  Returns NULL without a gfx950 device, for larger requests, or once
+ * the pool's range (EC_POOL_MB, default 2048 MiB) is used up -- the caller
+ * then allocates as it would without the pool. */
+void *ec_method_buffer_get(size_t bytes);
+/* Release a buffer: returns 1 when p came from ec_method_buffer_get (it is
+ * back in the pool), 0 when it did not (the caller frees it). */
+int32_t ec_method_buffer_put(void *p);
+
+/* Host-call crossover probes (tests and tuning; no device needed).
+ * ec_method_xover_route: would a host call of a volume with k data bricks go
+ * to the CPU engine (1) or a GPU (0)?  op 0 = encode, 1 = decode-type; user
+ * = user bytes, moved = bytes read + written, staged = bytes of its buffers
+ * that are not pinned and mapped, inflight = bytes queued on the GPU.
+ * ec_method_xover_observe feeds the router one completed call (engine 0 =
+ * CPU, 1 = GPU with every buffer mapped, 2 = every buffer staged, 3 = some of
+ * each; ns = its duration), as the library does after calls of >= 256 KiB;
+ * ec_method_xover_reset forgets every observation.  -EINVAL on bad args. */
+int32_t ec_method_xover_route(uint32_t k, int32_t op, uint64_t user, uint64_t moved,
+                              uint64_t staged, uint64_t inflight);
+int32_t ec_method_xover_observe(int32_t engine, int32_t op, uint32_t k, uint64_t user,
+                                uint64_t ns);
+void ec_method_xover_reset(void);
+
+/* Pool and deferred-registration counters (times in microseconds). */
+typedef struct {
+    uint64_t pool_bytes;           /* pinned bytes the pool has grown to      */
+    uint64_t in_use_bytes;         /* of which handed out now (class sizes)   */
+    uint64_t gets;                 /* ec_method_buffer_get calls              */
+    uint64_t misses;               /* of which returned NULL                  */
+    uint64_t slabs;                /* slabs registered                        */
+    uint64_t slab_register_us;     /* time to map, fault in and register them */
+    uint64_t deferred_registers;   /* ranges registered by the library thread */
+    uint64_t deferred_register_us; /* hipHostRegister time of those           */
+    uint64_t deferred_register_failures;
+    uint64_t unregisters;          /* ec_method_host_unregister calls done    */
+    uint64_t unregister_us;        /* hipHostUnregister time of those         */
+} ec_method_pool_stats_t;
+void ec_method_pool_stats(ec_method_pool_stats_t *stats);
 
 /* Host-side matrix helpers, exported for tests and tools: the n x k encode
  * matrix (ec-method.c:22-36) and the k x k inverse for ascending rows

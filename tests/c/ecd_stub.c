@@ -3,6 +3,7 @@
  * paths.  Every entry point of glusterfs_amd/csrc/ec_device.h. */
 #include <errno.h>
 #include <stddef.h>
+#include <string.h>
 
 #include "../../glusterfs_amd/csrc/ec_device.h"
 
@@ -34,6 +35,11 @@ void *ecd_host_alloc(size_t b) { (void)b; return NULL; }
 void ecd_host_free(void *p) { (void)p; }
 int ecd_host_register(void *p, size_t b) { (void)p; (void)b; return -ENODEV; }
 int ecd_host_unregister(void *p) { (void)p; return -ENODEV; }
+int ecd_host_register_async(void *p, size_t b) { (void)p; (void)b; return -ENODEV; }
+void ecd_host_register_flush(void) {}
+void *ecd_buffer_get(size_t b) { (void)b; return NULL; }
+int ecd_buffer_put(void *p) { (void)p; return 0; }
+void ecd_pool_stats(ecd_pool_stats_t *s) { memset(s, 0, sizeof(*s)); }
 uint64_t ecd_host_inflight(void) { return UINT64_MAX; }
 void ecd_inject_faults(uint32_t n) { (void)n; }
 int ecd_host_mapped(const void *p, size_t n) { (void)p; (void)n; return 0; }

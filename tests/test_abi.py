@@ -38,6 +38,16 @@ def test_library_exports_every_declared_symbol():
         assert getattr(lib, s)
 
 
+def test_library_is_not_unloadable():
+    """The library owns registered host memory, a registration thread and
+    the free hook the integration patch installs in libglusterfs's iobuf
+    layer (iobuf_set_data_allocator keeps it for buffers still out), so it
+    is linked -z nodelete: dlclose of the ec xlator must not unmap it."""
+    out = subprocess.run(["readelf", "-d", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    assert "NODELETE" in out, out
+
+
 def test_reference_prototypes_unchanged():
     """The five drop-in prototypes are those of ec-method.h:31-46."""
     text = " ".join(open(HDR).read().split())
@@ -89,6 +99,28 @@ def test_python_init_without_gpu_selects_cpu_engine():
         assert L.engine.startswith("cpu/")
     with g.ECMatrixList(4, 6, gen="hip") as L:
         assert L.engine.startswith("cpu/")
+
+
+def test_pool_and_deferred_registration_without_gpu():
+    """Without a device the pinned pool hands out nothing (the integration
+    patch's iobuf allocator then falls back to GF_MALLOC / GF_CALLOC), puts
+    of foreign pointers are refused (the caller frees them), and deferred
+    registration reports -ENODEV."""
+    import errno
+    import glusterfs_amd as g
+    if g.device_count() > 0:
+        pytest.skip("GPU visible")
+    L = g.ec_method.lib
+    assert not L.ec_method_buffer_get(1 << 20)
+    buf = (ctypes.c_uint8 * 4096)()
+    assert L.ec_method_buffer_put(ctypes.addressof(buf)) == 0
+    assert L.ec_method_buffer_put(None) == 0
+    assert L.ec_method_host_register_async(ctypes.addressof(buf), 4096) == -errno.ENODEV
+    L.ec_method_host_register_flush()
+    st = g.pool_stats()
+    assert st["pool_bytes"] == 0 and st["gets"] == 0 and st["deferred_registers"] == 0
+    b = g.PoolBuffer(8192)
+    assert not b.pooled and b.array.nbytes == 8192
 
 
 def test_host_matrices_match_oracle(oracle):

@@ -202,16 +202,25 @@ def test_large_calls_stream_outputs(ec, oracle, gen):
     nst = (16 << 20) // (CHUNK * k) + 3                  # > 16 MiB of decode output
     data = rnd(CHUNK * k * nst, seed=91)
     want = oracle.encode(k, n, data, nthreads=8)
+    def aligned(nbytes):
+        # 64-byte aligned, so the streaming-store path is really taken
+        # (np.zeros bases are 16 bytes past a page)
+        raw = np.zeros(nbytes + 64, np.uint8)
+        off = (-raw.ctypes.data) % 64
+        buf = raw[off:off + nbytes]
+        assert buf.ctypes.data % 64 == 0
+        return buf
+
     with ec.ECMatrixList(k, n, gen=gen) as L:
-        frags = [np.zeros(CHUNK * nst, np.uint8) for _ in range(n)]
+        frags = [aligned(CHUNK * nst) for _ in range(n)]
         L.encode_batch(nst, data, frags)
         for i in range(n):
             assert np.array_equal(frags[i], want[i]), i
         rows = [3, 4, 5, 6]
-        out = np.zeros(data.size, np.uint8)
+        out = aligned(data.size)
         L.decode_batch(nst, 0x3C, rows, [want[r - 1] for r in rows], out)
         assert np.array_equal(out, data)
-        raw = np.zeros(data.size + 64, np.uint8)
-        odd = raw[8:8 + data.size]
+        raw = aligned(data.size + 64)
+        odd = raw[8:8 + data.size]               # misaligned: regular stores
         L.decode_batch(nst, 0x3C, rows, [want[r - 1] for r in rows], odd)
         assert np.array_equal(odd, data)

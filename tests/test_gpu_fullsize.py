@@ -13,7 +13,9 @@ loops, ec-method.c:394-433, at the sizes bench.py times.
   configs[2]  8+4 64K-stripe batch encode, decode 0xFF0 and 0xEB5
   configs[3]  16+4 2 GiB encode for rank 0 and rank 1 (the stream offset of a
               stripe-range partition), and rank 0 through the pinned-host
-              (PCIe) path; the 8 GiB job strong-split over 2/4/8 ranks
+              (PCIe) path; the one 8 GiB job (1,048,576 stripes) strong-split
+              over N = 2 ranks: slices 0 and 1 (4 GiB each) on this GPU
+              against tests/golden/gen_strong_sha.py's per-slice fixtures
   configs[4]  self-heal: 8+4 1 GiB with 16 masks in 1024-stripe groups, 16+4
               1 GiB with 64 masks (device decode-matrix table)
 """
@@ -110,6 +112,24 @@ def test_config3_16p4_2gib_rank_slices(ec, torch_cuda, rank):
     """configs[3]: 16+4, 2 GiB per GPU; rank 1's slice starts 2 GiB into the
     stream, so the fixture also pins the partition offset."""
     L, data, frags, nst, k, n = _encoded(ec, torch_cuda, "16+4_2GiB", rank)
+    with L:
+        pass
+    del data, frags
+    torch_cuda.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("rank", [0, 1])
+def test_config3_16p4_8gib_job_strong_n2_slices(ec, torch_cuda, rank):
+    """configs[3] as one fixed job (strong scaling, bench.py strong_job): the
+    1,048,576-stripe 16+4 job cut by dist.stripe_range into two 4 GiB slices;
+    each rank's slice input and its 20 fragment slices against the fixture
+    (its stream offset is slice 1's start)."""
+    from glusterfs_amd import dist
+    fx = FIX["16+4_8GiBjob_N2_r%d" % rank]
+    s0, s1 = dist.stripe_range(rank, 2, fx["job_stripes"])
+    assert (s1 - s0) * CHUNK * fx["k"] == fx["bytes"]
+    assert s0 * CHUNK * fx["k"] // 8 == fx["word0"]
+    L, data, frags, nst, k, n = _encoded(ec, torch_cuda, "16+4_8GiBjob_N2", rank)
     with L:
         pass
     del data, frags

@@ -6,8 +6,9 @@ ec_encode_vander (the kernel 2+1 uses by default);
 EC_MI355X_PATCACHE=0 uploads the device pattern table of every mixed call
 instead of caching it; EC_MI355X_LDSNT=1 stages these small calls with the
 non-temporal LDS-DMA loads that the library uses above 256 MiB of input;
-EC_MI355X_ZCDB=1 runs host-buffer combines (k <= 8) through the persistent
-double-buffered zero-copy kernel instead of one tile per block.
+EC_MI355X_ZCDB=0 runs host-buffer combines (k <= 8) through the one tile per
+block zero-copy kernel instead of the persistent double-buffered one (the
+default since r04; =1 forces it), each with host decode, heal and mixed calls.
 Each runs here in its own process through the C ABI, bit-exact against the
 oracle on device-resident encode, full / partial decode (ragged tiles
 included) and mixed decode.
@@ -80,11 +81,30 @@ for k, n in ((4, 6), (8, 12), (16, 20)):
                 L.decode_batch(nst, m, rows, [frags[r - 1] for r in rows], out)
                 exp = O.decode(k, rows, [frags[r - 1] for r in rows])
                 assert np.array_equal(out, exp), ("host dec", k, n, nst, hex(m))
+            # host heal (fragment-major output rows) and a host mixed decode
+            m = masks[1]
+            rows = O.mask_rows(m)
+            tgt = [b for b in range(n) if not (m >> b) & 1][:2]
+            tmask = sum(1 << b for b in tgt)
+            hout = [np.empty(512 * nst, np.uint8) for _ in tgt]
+            L.heal(nst, m, [frags[r - 1] for r in rows], tmask, hout)
+            data = O.decode(k, rows, [frags[r - 1] for r in rows])
+            full = O.encode(k, n, data)
+            for j, b in enumerate(tgt):
+                assert np.array_equal(hout[j], full[b]), ("host heal", k, n, nst, b)
+            grp = 4 if nst % 4 == 0 else 1
+            gm = [masks[(i * 7) % 4] for i in range((nst + grp - 1) // grp)]
+            L.decode_mixed(nst, grp, gm, frags, out)
+            for gi, gmask in enumerate(gm):
+                rws = O.mask_rows(gmask)
+                a0, a1 = gi * grp * 512, min(nst, (gi + 1) * grp) * 512
+                exp = O.decode(k, rws, [frags[r - 1][a0:a1] for r in rws])
+                assert np.array_equal(out[a0 * k:a1 * k], exp), ("host mixed", k, n, nst, gi)
 print("ok")
 """
 
 KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1"),
-         ("EC_MI355X_ZCDB", "1")]
+         ("EC_MI355X_ZCDB", "0"), ("EC_MI355X_ZCDB", "1")]
 
 
 @pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])
@@ -92,5 +112,5 @@ def test_ab_instantiation_bit_exact(knob, value):
     env = dict(os.environ, EC_MI355X_QUIET="1", EC_GPU_ALWAYS="1")
     env[knob] = value
     r = subprocess.run([sys.executable, "-c", SCRIPT], cwd=ROOT, env=env, capture_output=True,
-                       text=True, timeout=110)
+                       text=True, timeout=170)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]

@@ -96,8 +96,63 @@ def test_patched_iobuf_arena_hooks(scratch):
     assert "typedef int (*iobuf_arena_hook_t)(void *base, size_t size);" in hdr
     assert "iobuf_set_arena_hooks\n" in (scratch / LIBSRC / "libglusterfs.sym").read_text()
     ec = (scratch / SUB / "ec.c").read_text()
-    assert "ec_method_host_register(base, size)" in ec
+    # registration is deferred to the library's thread: the arena hook runs
+    # under iobuf_pool->mutex (VERDICT r03 missing #1)
+    assert "ec_method_host_register_async(base, size)" in ec
+    assert "ec_method_host_register(base" not in ec
     assert "ec_method_host_unregister(base)" in ec
-    assert "ec->iobuf_hooks = ec_iobuf_hooks_get(this, extensions);" in ec
+    assert "ec->iobuf_hooks = ec_iobuf_hooks_get(this, &ec->matrix);" in ec
     assert "ec_iobuf_hooks_put(this);" in ec
     assert "gf_boolean_t iobuf_hooks;" in (scratch / SUB / "ec-types.h").read_text()
+
+
+def _c_body(src, name):
+    """Text of the C function `name` (definition at column 0 to its closing
+    brace at column 0)."""
+    i = src.index("\n%s(" % name) + 1
+    return src[i:src.index("\n}\n", i) + 2]
+
+
+def test_patched_iobuf_data_allocator_covers_every_size_class(scratch):
+    """VERDICT r03 missing #1: ec_buffer_alloc (ec-helpers.c:134-165) ->
+    iobuf_get_page_aligned -> iobuf_get2 (iobuf.c:513-569) serves a request
+    from one of three places, and every one must reach the coder's pinned
+    memory: <= 128 KiB GF_MALLOC (iobuf_get_from_small), > 1 MiB GF_CALLOC
+    (iobuf_get_from_stdalloc) -- both now ask the data allocator first --
+    and the arenas in between (registered by the arena hooks).  Frees of
+    those buffers go back through the allocator's free hook."""
+    subprocess.run(["patch", "-p1", "--batch", "-i", PATCH], cwd=scratch, check=True,
+                   capture_output=True)
+    io = (scratch / LIBSRC / "iobuf.c").read_text()
+    # the size split of iobuf_get2 is the reference's, untouched
+    get2 = _c_body(io, "iobuf_get2")
+    assert "page_size <= USE_IOBUF_POOL_IF_SIZE_GREATER_THAN" in get2
+    assert "iobuf_get_from_small(page_size)" in get2
+    assert "iobuf_get_from_stdalloc(iobuf_pool, page_size)" in get2
+    assert "__iobuf_get(iobuf_pool, rounded_size, index)" in get2
+    # <= 128 KiB: the allocator first, GF_MALLOC when it declines
+    small = _c_body(io, "iobuf_get_from_small")
+    a, m = small.index("data_alloc(page_size)"), small.index("GF_MALLOC(page_size")
+    assert a < m and "if (!iobuf->free_ptr)" in small[a:m]
+    # > 1 MiB: the allocator first, GF_CALLOC when it declines
+    std = _c_body(io, "iobuf_get_from_stdalloc")
+    a, c = std.index("data_alloc((page_size + GF_IOBUF_ALIGN_SIZE) - 1)"), std.index("GF_CALLOC(\n")
+    assert a < c
+    # every free of a non-arena iobuf asks the free hook before GF_FREE
+    fr = _c_body(io, "__iobuf_free")
+    assert fr.index("data_free(iobuf->free_ptr)") < fr.index("GF_FREE(iobuf->free_ptr)")
+    assert "iobuf_set_data_allocator(struct iobuf_pool *iobuf_pool" in io
+    # 128 KiB < size <= 1 MiB: arena pages, registered after the mmap
+    assert "iobuf_arena_reg(iobuf_arena->mem_base" in _c_body(io, "__iobuf_arena_alloc")
+    hdr = (scratch / LIBSRC / "glusterfs" / "iobuf.h").read_text()
+    assert "typedef void *(*iobuf_data_alloc_t)(size_t size);" in hdr
+    assert "typedef int (*iobuf_data_free_t)(void *ptr);" in hdr
+    assert "iobuf_set_data_allocator\n" in (scratch / LIBSRC / "libglusterfs.sym").read_text()
+    ec = (scratch / SUB / "ec.c").read_text()
+    assert "ec_method_buffer_get(size)" in ec and "ec_method_buffer_put(ptr)" in ec
+    get = _c_body(ec, "ec_iobuf_hooks_get")
+    assert "iobuf_set_data_allocator(this->ctx->iobuf_pool, ec_iobuf_data_alloc," in get
+    put = _c_body(ec, "ec_iobuf_hooks_put")
+    # the free hook is kept when the last volume goes (buffers still out)
+    assert "iobuf_set_data_allocator(this->ctx->iobuf_pool, NULL,\n" in put
+    assert "ec_iobuf_data_free);" in put

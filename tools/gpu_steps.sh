@@ -5,7 +5,7 @@
 # Steps: smoke | pytest | pytest_new (the files in $TESTS) | bench | bench_rocprof
 #        | rehearsal (2 gloo ranks on GPU 0) | profile (per-config rocprof + PMC)
 #        | kbench (tools/kbench/kbench $KBENCH_ARGS) | kb3 (tools/kbench/kb3 $KB3_ARGS)
-#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
+#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
 # Logs go to gpurun_out/${TAG}_<step>.log.
 set -u
 mkdir -p gpurun_out
@@ -34,6 +34,7 @@ for step in "$@"; do
     zcsizes) run zcsizes 600 bash -c 'for r in 1 2; do for v in 0 1; do EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v python3 tools/zc_sizes.py || exit 1; done; done' ;;
     hsweep) run hsweep 300 bash -c "cd /tmp && export TMPDIR=/tmp && EC_GPU_ALWAYS=1 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_hsweep_$TAG -o run --output-format csv -- python3 $R/bench.py --heal-sweep gpu --steps 64 && python3 $R/tools/prof_filter.py $R/gpurun_out/prof_hsweep_$TAG ec_ && python3 $R/tools/trace_seq.py $R/gpurun_out/prof_hsweep_$TAG" ;;
     hostlat) run hostlat 180 python -u tools/host_latency.py ;;
+    hsweep3) run hsweep3 400 bash -c 'for m in auto gpu cpu; do echo "== $m"; if [ $m = gpu ]; then E=1; else E=0; fi; EC_GPU_ALWAYS=$E python3 bench.py --heal-sweep $m --steps 64 || exit 1; done' ;;
     kb3) run kb3 600 tools/kbench/kb3 ${KB3_ARGS:-1 7 all} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
