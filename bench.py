@@ -421,6 +421,10 @@ def extra_configs(c, steps, warmup):
         ex["heal_sweep_8+4_4MiB_windows"] = heal_sweep_all()
     except Exception as exc:                     # reported, never fatal to the bench line
         ex["heal_sweep_8+4_4MiB_windows"] = dict(error=repr(exc)[:200])
+    try:
+        ex["concurrency_8+4_batching_ceiling"] = concurrency_probe()
+    except Exception as exc:                     # reported, never fatal to the bench line
+        ex["concurrency_8+4_batching_ceiling"] = dict(error=repr(exc)[:200])
     ex["fullsize_sha256_checks"] = dict(c.checks)
     return ex
 
@@ -580,10 +584,14 @@ def heal_sweep(mode, windows=64):
     return res
 
 
-def heal_sweep_all(windows=64):
+def heal_sweep_all(windows=256):
     import subprocess
     out = dict(windows=windows, window_bytes=4 << 20,
-               calls="per window: ec_method_decode (8 of 12 fragments) + ec_method_encode")
+               calls="per window: ec_method_decode (8 of 12 fragments) + ec_method_encode",
+               provenances="pageable: plain malloc; registered: one registered region; "
+                           "ec_provenance: the integration patch (fragments in deferred-registered "
+                           "1 MiB-page arenas, outputs from the pinned pool); "
+                           "ec_provenance_calloc: registered fragments, calloc outputs")
     for mode in ("auto", "gpu", "cpu"):
         env = dict(os.environ)
         env.pop("EC_GPU_ALWAYS", None)
@@ -595,6 +603,35 @@ def heal_sweep_all(windows=64):
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
         out[mode] = json.loads(line[-1]) if r.returncode == 0 and line else dict(
             error=(r.stderr or r.stdout)[-300:])
+    return out
+
+
+def concurrency_probe(secs=0.5):
+    """The batching-queue question: 8 threads of
+    4 MiB 8+4 heal windows and 16 threads of 128 KiB writes / reads through the
+    drop-in API on pool buffers (the patched client's iobufs), each timed as
+    concurrent calls, as ONE call carrying all their bytes (the ceiling of any
+    coalescing queue) and serially -- tools/kbench/concur (C threads: Python's
+    per-call overhead would swamp 4 us CPU calls), per engine setting."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "kbench", "concur")
+    if not os.path.exists(exe):
+        return dict(error="tools/kbench/concur not built (make -C glusterfs_amd tools)")
+    out = {}
+    for mode, gen, always in (("auto", "auto", "0"), ("gpu", "auto", "1"), ("cpu", "avx", "0")):
+        env = dict(os.environ, EC_GPU_ALWAYS=always, EC_MI355X_QUIET="1")
+        r = subprocess.run([exe, str(secs), gen, "pool"], env=env, capture_output=True, text=True,
+                           timeout=240)
+        for line in r.stdout.splitlines():
+            if line.startswith("{"):
+                d = json.loads(line)
+                key = "%s_%s" % (d["scenario"], mode)
+                out.setdefault(key, {})[d["way"]] = dict(
+                    user_GBps=d["user_GBps"], p50_us=d["p50_us"], threads=d["threads"],
+                    call_KiB=d["call_KiB"], gpu_calls=d["gpu_calls"], cpu_calls=d["cpu_calls"],
+                    ok=d["ok"])
+        if r.returncode != 0:
+            out["error_" + mode] = (r.stderr or r.stdout)[-300:]
     return out
 
 

@@ -324,12 +324,41 @@ class CopyPool {
 
 CopyPool g_copy_pool;
 
-/* Split [dst, src, n) copies into ~2 MiB pieces for the pool. */
+/* Split [dst, src, n) copies into pieces for the pool: n / copy threads,
+ * between 256 KiB and 2 MiB (64 KiB multiples).  Fixed 2 MiB pieces left a
+ * 4 MiB heal-window output on two of the eight threads (r04: a registered-
+ * fragment decode into a pageable output took 323 us against 185 us with
+ * every buffer mapped, bench.py heal_sweep ec_provenance_calloc). */
 void add_copy(std::vector<CopyPool::Piece> &v, uint8_t *dst, const uint8_t *src, size_t n)
 {
-    constexpr size_t kPiece = 2u << 20;
-    for (size_t o = 0; o < n; o += kPiece)
-        v.push_back({dst + o, src + o, std::min(kPiece, n - o)});
+    const size_t t = (size_t)std::max(1, copy_threads());
+    const size_t piece =
+        std::min<size_t>(2u << 20, std::max<size_t>(256u << 10, (n / t + 0xFFFF) & ~(size_t)0xFFFF));
+    for (size_t o = 0; o < n; o += piece)
+        v.push_back({dst + o, src ? src + o : nullptr, std::min(piece, n - o)});
+}
+
+/* Stripes per pipeline batch of a call that stages some of its buffers:
+ * `full` (the batch sized by pipe_batch_bytes), but a call of a single such
+ * batch is cut into up to 4 batches of >= 1 MiB of input, so the copies of
+ * one batch overlap the kernel of the next (a 4 MiB heal window was one
+ * batch: copy in, kernel, copy out, strictly in turn).  `in_stripe` = input
+ * bytes per stripe, `unit` = stripes the batches must be a multiple of. */
+uint64_t staged_batch(uint64_t full, uint64_t cnt_all, uint64_t in_stripe, uint64_t unit)
+{
+    static const int split = [] {              /* EC_PIPE_SPLIT=1: one batch (A/B) */
+        const char *e = getenv("EC_PIPE_SPLIT");
+        return e ? atoi(e) : 4;
+    }();
+    if (split <= 1 || cnt_all > full)
+        return full;
+    const uint64_t min_st = std::max<uint64_t>(1, (1u << 20) / in_stripe);
+    uint64_t nb = std::min<uint64_t>((uint64_t)split, cnt_all / min_st);
+    if (nb <= 1)
+        return full;
+    uint64_t b = (cnt_all + nb - 1) / nb;
+    b = (b + unit - 1) / unit * unit;
+    return std::max<uint64_t>(b, unit);
 }
 
 /* A virtual input made of consecutive segments (nullptr = zeros): the
@@ -528,24 +557,29 @@ class BufPool {
 
     void *get(size_t bytes)
     {
-        if (bytes == 0 || bytes > (size_t)kMaxRun * kGran || !ready())
+        if (!ready())
             return nullptr;
         gets_.fetch_add(1, std::memory_order_relaxed);
-        const int c = cls(bytes);
-        {
-            std::lock_guard<std::mutex> g(mu_[c]);
-            if (!free_[c].empty()) {
-                void *p = free_[c].back();
-                free_[c].pop_back();
-                in_use_.fetch_add(csize(c), std::memory_order_relaxed);
-                return p;
-            }
-        }
-        if (!grow(c)) {
+        if (bytes == 0 || bytes > (size_t)kMaxRun * kGran) {
             misses_.fetch_add(1, std::memory_order_relaxed);
             return nullptr;
         }
-        return get(bytes);
+        const int c = cls(bytes);
+        for (;;) {
+            {
+                std::lock_guard<std::mutex> g(mu_[c]);
+                if (!free_[c].empty()) {
+                    void *p = free_[c].back();
+                    free_[c].pop_back();
+                    in_use_.fetch_add(csize(c), std::memory_order_relaxed);
+                    return p;
+                }
+            }
+            if (!grow(c)) {    /* (another thread may take the new slab: retry) */
+                misses_.fetch_add(1, std::memory_order_relaxed);
+                return nullptr;
+            }
+        }
     }
 
     /* true when p is a buffer of the pool (now free again) */
@@ -1025,8 +1059,10 @@ int run_encode_dev(int dev, const EncodeJob &j)
         all_direct &= out_direct[i];
     }
     /* fully mapped jobs still run in batches so one launch stays short */
-    const uint64_t B = std::min<uint64_t>(
+    uint64_t B = std::min<uint64_t>(
         cnt_all, std::max<uint64_t>(1, (all_direct ? 8 : 1) * pipe_batch_bytes() / stripe_in));
+    if (!all_direct)
+        B = std::min<uint64_t>(cnt_all, staged_batch(B, cnt_all, stripe_in, 1));
     Stage *s = acquire(dev);
     if (!s)
         return -EIO;
@@ -1097,6 +1133,8 @@ int run_decode_dev(int dev, const DecodeJob &j)
     uint64_t B = std::max<uint64_t>(
         1, (all_direct ? 8 : 1) * pipe_batch_bytes() / ((uint64_t)j.nfrags * ECD_CHUNK));
     const uint64_t grp = j.group_pattern ? (1ull << j.group_shift) : 1;
+    if (!all_direct)
+        B = staged_batch(B, cnt_all, (uint64_t)j.nfrags * ECD_CHUNK, 1);
     if (j.group_pattern)
         B = std::max<uint64_t>(grp, B / grp * grp);
     /* batches start at multiples of B (whole groups), but the staging slots

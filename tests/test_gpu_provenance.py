@@ -91,6 +91,7 @@ def test_pool_buffers_classes_and_recycling(ec):
     assert lib.ec_method_buffer_put(bufs[0] + 64) == 0             # inside, not a buffer
     st1 = ec.pool_stats()
     assert st1["gets"] - st0["gets"] == 2 * len(sizes) + 1
+    assert st1["misses"] - st0["misses"] == 1                     # the 128 MiB + 1 request
     assert st1["in_use_bytes"] == st0["in_use_bytes"]
     assert st1["slabs"] >= 1 and st1["pool_bytes"] >= (128 << 20)
 

@@ -5,7 +5,7 @@
 # Steps: smoke | pytest | pytest_new (the files in $TESTS) | bench | bench_rocprof
 #        | rehearsal (2 gloo ranks on GPU 0) | profile (per-config rocprof + PMC)
 #        | kbench (tools/kbench/kbench $KBENCH_ARGS) | kb3 (tools/kbench/kb3 $KB3_ARGS)
-#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
+#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | concur (tools/kbench/concur: concurrent vs coalesced-ceiling calls, auto / gpu / cpu) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
 # Logs go to gpurun_out/${TAG}_<step>.log.
 set -u
 mkdir -p gpurun_out
@@ -30,11 +30,12 @@ for step in "$@"; do
     profile) run profile 900 bash tools/profile.sh "$TAG" ${PROFILE_ARGS:-dec:4+2:3C 1 enc:4+2 1 enc:8+4 0.25 dec:8+4:FF0 0.25 enc:16+4 2 mixed:8+4 1 heal:8+4 1 dec:16+4:FFFF0 1 mixed:16+4:64 1 rmw:4+2 1} ;;
     kbench) run kbench 600 tools/kbench/kbench ${KBENCH_ARGS:-} ;;
     trace) run trace 600 bash tools/prof_trace.sh "$TAG" ${TRACE_ARGS:-dec:16+4:FFFF0 1 dec:4+2:3C 1} ;;
-    zcab) run zcab 600 bash -c 'for r in 1 2 3; do for v in 0 1; do echo "== round $r EC_MI355X_ZCDB=$v"; EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v python3 bench.py --heal-sweep gpu --steps 64 || exit 1; done; done' ;;
+    zcab) run zcab 600 bash -c 'for r in 1 2 3; do for v in 0 1; do echo "== round $r EC_MI355X_ZCDB=$v"; EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v python3 bench.py --heal-sweep gpu --steps 256 || exit 1; done; done' ;;
     zcsizes) run zcsizes 600 bash -c 'for r in 1 2; do for v in 0 1; do EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v python3 tools/zc_sizes.py || exit 1; done; done' ;;
     hsweep) run hsweep 300 bash -c "cd /tmp && export TMPDIR=/tmp && EC_GPU_ALWAYS=1 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_hsweep_$TAG -o run --output-format csv -- python3 $R/bench.py --heal-sweep gpu --steps 64 && python3 $R/tools/prof_filter.py $R/gpurun_out/prof_hsweep_$TAG ec_ && python3 $R/tools/trace_seq.py $R/gpurun_out/prof_hsweep_$TAG" ;;
     hostlat) run hostlat 180 python -u tools/host_latency.py ;;
-    hsweep3) run hsweep3 400 bash -c 'for m in auto gpu cpu; do echo "== $m"; if [ $m = gpu ]; then E=1; else E=0; fi; EC_GPU_ALWAYS=$E python3 bench.py --heal-sweep $m --steps 64 || exit 1; done' ;;
+    concur) run concur 400 bash -c 'EC_GPU_ALWAYS=0 tools/kbench/concur ${CONCUR_SECS:-1} auto && EC_GPU_ALWAYS=1 tools/kbench/concur ${CONCUR_SECS:-1} auto && EC_GPU_ALWAYS=0 tools/kbench/concur ${CONCUR_SECS:-1} avx' ;;
+    hsweep3) run hsweep3 400 bash -c 'for m in auto gpu cpu; do echo "== $m"; if [ $m = gpu ]; then E=1; else E=0; fi; EC_GPU_ALWAYS=$E python3 bench.py --heal-sweep $m --steps 256 || exit 1; done' ;;
     kb3) run kb3 600 tools/kbench/kb3 ${KB3_ARGS:-1 7 all} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
