@@ -63,6 +63,9 @@ def parse():
                     help="N > 1: skip the per-N 16+4 encode / self-heal / PCIe lines")
     ap.add_argument("--heal-sweep", default=None, choices=("auto", "gpu", "cpu"),
                     help="child mode of the heal-sweep extra: one engine setting, JSON out")
+    ap.add_argument("--warm-ms", type=float, default=0.0,
+                    help="--only: keep launching for this long before the timed launches "
+                         "(past the first ~10 ms clock transient of a compute-heavy kernel)")
     ap.add_argument("--only", default=None,
                     help="profiling helper: enc:K+R | dec:K+R:MASKHEX | mixed:K+R[:NMASKS[:GROUP]] | heal:K+R | "
                          "rmw:K+R")
@@ -924,6 +927,7 @@ def main():
     c = Ctx(g, torch, dev, grp.rank)
     nbytes = int(args.gib * (1 << 30))
     if args.only:
+        c.warm_ms = args.warm_ms
         return only(c, args.only, nbytes, args.steps, args.warmup)
 
     k, n, mask = 4, 6, 0x3C

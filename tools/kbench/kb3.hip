@@ -373,6 +373,100 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_db(const CombineArgs a)
     }
 }
 
+/* Persistent k = 16 combine with deferred stores (r04 candidate, VERDICT r03
+ * #5: the compute phase and the HBM phases add up instead of overlapping).
+ * One 64 KiB tile per block, as ec_combine (so two blocks still share a CU),
+ * but each block walks tiles blockIdx.x, + gridDim.x, ... and, once every
+ * wave has read tile t (barrier), issues the staging of tile t + 1 into the
+ * same LDS and only then the stores of tile t's row from its registers: the
+ * block's reads and writes are in flight together, and the stores drain
+ * under the next tile's compute.  Waits are counted: per wave 4 LDS-DMA
+ * instructions (missing stripes' addresses clamped, never skipped), then 4
+ * 16-byte stores (a full tile: every tile but the grid's last), so
+ * vmcnt(4) retires exactly the staging.  LDS reads in asm (the compiler
+ * would put vmcnt(0) before a ds_read behind pending LDS-DMA). MIX = the
+ * tile's pattern from the group map (kernel-argument patterns). */
+template <bool NTS, int LA, bool MIX = false>
+__global__ __launch_bounds__(16 * 64) void ec_combine_pd(const CombineArgs a)
+{
+    constexpr u32 T = 8, K = 16, NW = 16;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    const uint64_t ntiles = (a.nstripes + T - 1) / T;
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles)
+        return;
+    const uint64_t last = a.nstripes - 1;
+    auto stage = [&](uint64_t tile) {
+        const PatWords<false> pw(a, tile_pattern<MIX>(a, tile * T), lane, nullptr);
+#pragma unroll
+        for (u32 j = 0; j < 4; ++j) {
+            const u32 ins = j * NW + wave;
+            const u32 p = ins / (T / 2);
+            const u32 el = (ins * 64 + lane) % (T * 32);
+            uint64_t st = tile * T + (el >> 2) % T;
+            st = st < last ? st : last;
+            const uint8_t *g = a.in_base[pw.byte(a, p)] + st * a.in_stride + ((el >> 2) / T) * 64u +
+                               (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, LA);
+        }
+    };
+    const u32 r = wave;
+    const bool has = r < a.rows;                     /* wave-uniform */
+    const u32 cs = lane >> 3, cc = lane & 7u;
+    const uint8_t *col = lds + cs * 64u + cc * 8u;
+    stage(t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (;;) {
+        u32 acc[8][2], y[8][2];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc[b][0] = acc[b][1] = 0;
+        if (has) {
+            const PatWords<false> pw(a, tile_pattern<MIX>(a, t * T), lane, nullptr);
+            const u32 rw = a.kw * (1 + r);
+            uint64_t cl = (uint64_t)pw.word(a, rw) | ((uint64_t)pw.word(a, rw + 1) << 32);
+            uint64_t ch = (uint64_t)pw.word(a, rw + 2) | ((uint64_t)pw.word(a, rw + 3) << 32);
+#pragma unroll 1
+            for (u32 p = 0; p < K; ++p) {
+                const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
+                cl = (cl >> 8) | (ch << 56);
+                ch >>= 8;
+                if (c == 0)                          /* ec-code-c.c:11666-11676 */
+                    continue;
+                lds_read_planes_b64(col + p * (T * ECD_CHUNK), y);
+                ecgf::mul_xor_jt<2>(c, acc, y);
+            }
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();                /* tile t read by every wave */
+        asm volatile("" ::: "memory");
+        const uint64_t tn = t + gridDim.x;
+        const bool more = tn < ntiles;
+        if (more)
+            stage(tn);
+        const uint64_t ost = t * T + cs;
+        if (has)
+            store_chunk_pairs<NTS>(a.out_base[r] + (ost < a.nstripes ? ost : 0) * a.out_stride, cc,
+                                   acc, ost < a.nstripes);
+        if (!more)
+            break;
+        if (has)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   /* staging in, stores may fly */
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                /* tile t + 1 in LDS */
+        asm volatile("" ::: "memory");
+        t = tn;
+    }
+}
+
 /* Where does the k = 16 decode's time go?  A copy of ec_combine's single-
  * pattern k = 16 path (8-stripe tile, 16 waves, CW = 2, jump table) with
  * the HBM sides removable: MODE bit 0 = no staging loads (compute on
@@ -707,6 +801,45 @@ int main(int argc, char **argv)
     };
     if (want(groups, "dec16"))
         decode_group(std::integral_constant<int, 16>{}, "decode 16+4 dense", false);
+    /* r04: the persistent deferred-store k = 16 combine against the shipped
+     * one, grids of 1 / 2 / 3 / 4 blocks per CU (two are resident) */
+    if (want(groups, "dec16pd")) {
+        constexpr int K = 16;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        uint8_t *fr[16];
+        for (int p = 0; p < K; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)(1 + (i * 173 + 11) % 255);
+        const CombineArgs *a = make_args(K, K, nst, fr, bufB, true, c);
+        const double bytes = (double)nst * 2 * K * ECD_CHUNK;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        const bool nt = nt_staging(nst * K * ECD_CHUNK);
+        add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
+        const uint64_t ntiles = (nst + 7) / 8;
+        for (int per : {2, 4, 8}) {
+            const uint64_t g = std::min<uint64_t>(ntiles, (uint64_t)per * prop.multiProcessorCount);
+            static char nm[3][64];
+            char *n = nm[per == 2 ? 0 : per == 4 ? 1 : 2];
+            snprintf(n, 64, "persistent deferred stores, grid %d/CU", per);
+            if (nt) {
+                auto kern = ec_combine_pd<true, kLdsDmaNT>;
+                lds_attr((const void *)kern, 64u << 10);
+                v.push_back({n, bytes, [=](hipStream_t st) {
+                                 hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * 16), 64u << 10, st, *a);
+                             }, bufB, ob});
+            } else {
+                auto kern = ec_combine_pd<true, kLdsDmaDefault>;
+                lds_attr((const void *)kern, 64u << 10);
+                v.push_back({n, bytes, [=](hipStream_t st) {
+                                 hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * 16), 64u << 10, st, *a);
+                             }, bufB, ob});
+            }
+        }
+        run_group("decode 16+4, persistent deferred stores (r04)", v, rounds, iters, s);
+        v.clear();
+    }
     /* Placement of the fragments: contiguous in one allocation (64 MiB apart
      * at 1 GiB), staggered by p * 4 KiB + p * 64 B, or one hipMalloc each
      * (as torch tensors are) -- the bench's k >= 8 decodes ran ~8-10 %

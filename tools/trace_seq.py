@@ -3,7 +3,7 @@
 rocprofv3 --kernel-trace output directory (after prof_filter.py):
 count, min / median / mean / max, and the sequence in groups of 10, so a
 slow start, a drift under sustained load or outliers show.
-Usage: trace_seq.py DIR [PATTERN]"""
+Usage: [LAST=N] trace_seq.py DIR [PATTERN]"""
 import csv
 import os
 import statistics
@@ -26,7 +26,10 @@ def main():
     by = {}
     for s, e, n in rows:
         by.setdefault(n, []).append((s, e))
+    last = int(os.environ.get("LAST", "0"))        # only the last N launches of each kernel
     for n, v in by.items():
+        if last:
+            v = v[-last:]
         d = [(e - s) / 1e3 for s, e in v]
         gaps = [(v[i + 1][0] - v[i][1]) / 1e3 for i in range(len(v) - 1)]
         print("%s\n  launches %d  min %.1f  med %.1f  mean %.1f  max %.1f us; gap med %.1f us"
