@@ -431,6 +431,65 @@ __device__ __forceinline__ void stage_tile(uint8_t *lds, A chunk, u32 k, uint64_
     }
 }
 
+constexpr u32 kNoStripe = 0xFFFFFFFFu;        /* padding slot            */
+constexpr uint64_t kNoSlot = ~0ull;            /* "no stripe here" in tiles */
+
+/* Make every value of `v` (wave-uniform: SGPRs) available at this point.
+ * Scalar loads return out of order, so the compiler waits lgkmcnt(0) before
+ * the first use of any of several in flight; left to itself it interleaved
+ * load, wait, use per element.  An empty asm that takes them all right after
+ * they are issued puts the one wait there and keeps the loads together. */
+template <typename V, size_t N>
+__device__ __forceinline__ void resolve_sgprs(V (&v)[N])
+{
+#pragma unroll
+    for (size_t i = 0; i < N; ++i)
+        asm volatile("" : "+s"(v[i]));
+}
+
+/* stage_tile for the combines, whose input bases are looked up (pattern
+ * src[] byte, then the in_base[] entry: two dependent scalar loads per
+ * input).  As stage_tile wrote it each staging instruction waited for its own
+ * pair, so a wave's 2-4 LDS-DMA issues sat behind 4-8 serialised scalar round
+ * trips at the head of every block.  Here the wave resolves the bases of all
+ * its instructions first (KMAX: the kernel's largest k; inputs past k are
+ * clamped, never staged), so the scalar loads overlap, then issues the
+ * staging.  base(p): input p's base (wave-uniform); stripe(slot): the stripe
+ * of tile slot `slot`, kNoSlot for none; slots >= nslots are skipped. */
+template <int KMAX, int T, int NW, int LA, typename B, typename S>
+__device__ __forceinline__ void stage_tile_b(uint8_t *lds, B base, S stripe, uint64_t in_stride,
+                                             u32 k, uint64_t t0, uint64_t nslots, u32 wave,
+                                             u32 lane)
+{
+    constexpr u32 PER = T / 2;                 /* wave instructions per input */
+    constexpr u32 MAXI = (KMAX * PER + NW - 1) / NW;
+    const u32 ni = k * PER;
+    const uint8_t *bp[MAXI];
+#pragma unroll
+    for (u32 i = 0; i < MAXI; ++i) {
+        const u32 ins = wave + i * NW;
+        const u32 p = ins < ni ? ins / PER : k - 1;
+        bp[i] = base(p);
+    }
+    resolve_sgprs(bp);
+#pragma unroll
+    for (u32 i = 0; i < MAXI; ++i) {
+        const u32 ins = wave + i * NW;
+        if (ins >= ni)
+            break;
+        const u32 el = (ins % PER) * 64 + lane;  /* 16-B piece within input p */
+        const u32 seg = el >> 2;
+        const uint64_t slot = t0 + seg % T;
+        const uint64_t st = slot < nslots ? stripe(slot) : kNoSlot;
+        if (st != kNoSlot) {
+            const uint8_t *g = bp[i] + st * in_stride + (seg / T) * 64u + (el & 3u) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)g,
+                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, LA);
+        }
+    }
+}
+
 /* wave-local LDS hand-off (the slice is private to the wave) */
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -859,28 +918,77 @@ constexpr u32 kMaxPatWords = 128; /* one pattern: kw * (1 + rows) <= 4 * 32 */
  * load per coefficient would need a vmcnt(0) wait that also drains the
  * outstanding stores; keeping the words in VGPRs cost the k = 16 kernel its
  * second block per CU: 68 VGPRs.) */
+/* A wave-uniform dword of read-only global memory by a scalar load (constant
+ * address space: s_load_dword through the scalar cache).  As a vector load
+ * it was global_load + s_waitcnt vmcnt(0) at the head of every block, before
+ * its first staging load could issue (the group map byte of a mixed call and
+ * the src[] words of a PG pattern: a full memory round trip, serialised,
+ * per 4-stripe tile; r04). */
+__device__ __forceinline__ u32 scalar_load_u32(const void *p)
+{
+    const uintptr_t a = (uintptr_t)p;
+    return *reinterpret_cast<const __attribute__((address_space(4))) u32 *>(a);
+}
+
 template <bool PG>
 struct PatWords {
     u32 pb;
     u32 s0, s1, s2, s3;          /* PG: the src[] words */
+    u32 v0, v1;                  /* PG: this lane's words of the pattern */
     const u32 *lp;               /* PG: the pattern in LDS */
     __device__ __forceinline__ PatWords(const CombineArgs &a, u32 pat, u32 lane, uint8_t *lds_pat)
     {
         pb = pat * a.pwords;
         if constexpr (PG) {
             const u32 *t = a.patg + pb;
-            const u32 v0 = lane < a.pwords ? t[lane] : 0u;
-            const u32 v1 = lane + 64u < a.pwords ? t[lane + 64u] : 0u;
-            s0 = __builtin_amdgcn_readlane(v0, 0);
-            s1 = __builtin_amdgcn_readlane(v0, 1);
-            s2 = __builtin_amdgcn_readlane(v0, 2);
-            s3 = __builtin_amdgcn_readlane(v0, 3);
-            u32 *w = reinterpret_cast<u32 *>(lds_pat);
-            if (threadIdx.x < 64u) {   /* wave 0; visible after the staging barrier */
+            /* the src[] words by one scalar load (the staging addresses need
+             * them first; pwords >= 2 kw, so 4 words stay in the pattern
+             * when kw >= 2, 2 when kw = 1); the whole pattern by vector
+             * loads whose LDS copy park() writes after the staging is
+             * issued (r04: written here, the copy's vmcnt(0) held back the
+             * staging of every block) */
+            if (a.kw >= 2) {
+                const v4u q = *reinterpret_cast<const __attribute__((address_space(4))) v4u *>(
+                    (uintptr_t)t);
+                s0 = q.x;
+                s1 = q.y;
+                s2 = a.kw > 2 ? q.z : 0u;
+                s3 = a.kw > 3 ? q.w : 0u;
+            } else {
+                const v2u q = *reinterpret_cast<const __attribute__((address_space(4))) v2u *>(
+                    (uintptr_t)t);
+                s0 = q.x;
+                s1 = s2 = s3 = 0u;
+            }
+            v0 = lane < a.pwords ? t[lane] : 0u;
+            v1 = lane + 64u < a.pwords ? t[lane + 64u] : 0u;
+            lp = reinterpret_cast<const u32 *>(lds_pat);
+        }
+    }
+    /* PG: the pattern into LDS (wave 0), after the staging has been issued;
+     * visible to every wave after the staging barrier */
+    __device__ __forceinline__ void park(u32 lane) const
+    {
+        if constexpr (PG) {
+            u32 *w = const_cast<u32 *>(lp);
+            if (threadIdx.x < 64u) {
                 w[lane] = v0;
                 w[lane + 64u] = v1;
             }
-            lp = w;
+        }
+    }
+    /* the (up to 4) words of src[]: byte p of them is input p's source */
+    __device__ __forceinline__ void src_words(const CombineArgs &a, u32 (&w)[4]) const
+    {
+        if constexpr (PG) {
+            w[0] = s0;
+            w[1] = s1;
+            w[2] = s2;
+            w[3] = s3;
+        } else {
+#pragma unroll
+            for (u32 i = 0; i < 4; ++i)
+                w[i] = i < a.kw ? a.pat[pb + i] : 0u;
         }
     }
     /* (the argument struct is passed in, not held: holding a reference to
@@ -910,8 +1018,6 @@ struct PatWords {
 
 constexpr size_t kPatLdsBytes = kMaxPatWords * 4; /* PG kernels: LDS after the tile */
 
-constexpr u32 kNoStripe = 0xFFFFFFFFu;        /* padding slot            */
-constexpr uint64_t kNoSlot = ~0ull;            /* "no stripe here" in tiles */
 
 /* pattern id of the tile starting at stripe t0 (ids past the table clamp to
  * the last pattern: a bad caller map must not fault the device) */
@@ -920,7 +1026,11 @@ __device__ __forceinline__ u32 tile_pattern(const CombineArgs &a, uint64_t t0)
 {
     if constexpr (!MIXED)
         return 0u;
-    const u32 id = __builtin_amdgcn_readfirstlane(a.group_pattern[t0 >> a.group_shift]);
+    /* the aligned dword holding the byte, by a scalar load (an aligned dword
+     * never crosses a page, so it is mapped wherever the byte is) */
+    const uintptr_t ba = (uintptr_t)(a.group_pattern + (t0 >> a.group_shift));
+    const u32 w = scalar_load_u32(reinterpret_cast<const void *>(ba & ~(uintptr_t)3));
+    const u32 id = (w >> ((u32)(ba & 3u) * 8u)) & 0xFFu;
     return id < a.npatterns ? id : a.npatterns - 1u;
 }
 
@@ -1036,7 +1146,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     const u32 lane = tid & 63u;
     u32 nslots = 0;
     if constexpr (SLOTS) {
-        nslots = __builtin_amdgcn_readfirstlane(*a.slot_count);
+        nslots = scalar_load_u32(a.slot_count);
         if (t0 >= nslots)
             return;             /* the grid is sized for the worst padding */
     }
@@ -1069,6 +1179,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                 (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, LA);
         }
     }
+    pw.park(lane);
     __syncthreads();
 
     /* compute: (row, 8-stripe subtile) items spread over the NW waves */
@@ -1146,7 +1257,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
     const u32 lane = tid & 63u;
     u32 nslots = 0;
     if constexpr (SLOTS) {
-        nslots = __builtin_amdgcn_readfirstlane(*a.slot_count);
+        nslots = scalar_load_u32(a.slot_count);
         if (t0 >= nslots)
             return;             /* the grid is sized for the worst padding */
     }
@@ -1164,6 +1275,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
         const uint64_t st = slot_stripe<SLOTS>(a, slot, nslots);
         return st != kNoSlot ? a.in_base[pw.byte(a, p)] + st * a.in_stride : nullptr;
     }, k, t0, SLOTS ? (uint64_t)nslots : a.nstripes, wave, lane);
+    pw.park(lane);
     __syncthreads();
     const u32 cs = lane >> 4, cc = lane & 15u;
     const uint8_t *col = lds + cs * 64u + cc * 4u;

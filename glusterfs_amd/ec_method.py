@@ -17,7 +17,9 @@ import errno
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libec_mi355x.so")
+# EC_MI355X_LIB: another build of the same library (same-box A/B runs of two
+# builds, tools/ab_lib.sh); the product path is lib/libec_mi355x.so
+LIB_PATH = os.environ.get("EC_MI355X_LIB") or os.path.join(HERE, "lib", "libec_mi355x.so")
 
 EC_GF_BITS = 8
 EC_GF_MOD = 0x11D

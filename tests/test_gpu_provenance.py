@@ -235,3 +235,49 @@ def test_deferred_registration_queue(ec, oracle):
     assert st1["deferred_registers"] > st0["deferred_registers"]
     assert st1["deferred_register_failures"] == st0["deferred_register_failures"]
     assert st1["unregisters"] >= st0["unregisters"] + 1
+
+
+def test_pool_concurrent_get_put(ec):
+    """Eight threads take and return pool buffers of mixed size classes
+    (small slabs and granule runs) at once, each filling its buffer with its
+    own tag and checking it before the put: no buffer is ever handed to two
+    holders, and every get is matched by its put."""
+    import threading
+    lib = ec.ec_method.lib
+    sizes = [4096, 9000, 64 << 10, 200 << 10, 1 << 20, (2 << 20) + 5, (4 << 20) + 4159]
+    st0 = ec.pool_stats()
+    errors = []
+
+    def worker(tag):
+        rng = np.random.default_rng(tag)
+        held = []
+        try:
+            for it in range(300):
+                if held and (len(held) > 6 or rng.random() < 0.5):
+                    p, n = held.pop(int(rng.integers(len(held))))
+                    a = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p))
+                    if not (a[0] == tag and a[n - 1] == tag and a[n // 2] == tag):
+                        errors.append("buffer %#x of thread %d overwritten" % (p, tag))
+                    if lib.ec_method_buffer_put(p) != 1:
+                        errors.append("put refused %#x" % p)
+                else:
+                    n = sizes[int(rng.integers(len(sizes)))]
+                    p = lib.ec_method_buffer_get(n)
+                    if not p:
+                        errors.append("get(%d) failed" % n)
+                        continue
+                    ctypes.memset(p, tag, n)
+                    held.append((p, n))
+        finally:
+            for p, n in held:
+                lib.ec_method_buffer_put(p)
+
+    th = [threading.Thread(target=worker, args=(t + 1,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
+    st1 = ec.pool_stats()
+    assert st1["in_use_bytes"] == st0["in_use_bytes"]
+    assert st1["misses"] == st0["misses"]
