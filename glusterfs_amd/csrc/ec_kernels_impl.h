@@ -434,62 +434,6 @@ __device__ __forceinline__ void stage_tile(uint8_t *lds, A chunk, u32 k, uint64_
 constexpr u32 kNoStripe = 0xFFFFFFFFu;        /* padding slot            */
 constexpr uint64_t kNoSlot = ~0ull;            /* "no stripe here" in tiles */
 
-/* Make every value of `v` (wave-uniform: SGPRs) available at this point.
- * Scalar loads return out of order, so the compiler waits lgkmcnt(0) before
- * the first use of any of several in flight; left to itself it interleaved
- * load, wait, use per element.  An empty asm that takes them all right after
- * they are issued puts the one wait there and keeps the loads together. */
-template <typename V, size_t N>
-__device__ __forceinline__ void resolve_sgprs(V (&v)[N])
-{
-#pragma unroll
-    for (size_t i = 0; i < N; ++i)
-        asm volatile("" : "+s"(v[i]));
-}
-
-/* stage_tile for the combines, whose input bases are looked up (pattern
- * src[] byte, then the in_base[] entry: two dependent scalar loads per
- * input).  As stage_tile wrote it each staging instruction waited for its own
- * pair, so a wave's 2-4 LDS-DMA issues sat behind 4-8 serialised scalar round
- * trips at the head of every block.  Here the wave resolves the bases of all
- * its instructions first (KMAX: the kernel's largest k; inputs past k are
- * clamped, never staged), so the scalar loads overlap, then issues the
- * staging.  base(p): input p's base (wave-uniform); stripe(slot): the stripe
- * of tile slot `slot`, kNoSlot for none; slots >= nslots are skipped. */
-template <int KMAX, int T, int NW, int LA, typename B, typename S>
-__device__ __forceinline__ void stage_tile_b(uint8_t *lds, B base, S stripe, uint64_t in_stride,
-                                             u32 k, uint64_t t0, uint64_t nslots, u32 wave,
-                                             u32 lane)
-{
-    constexpr u32 PER = T / 2;                 /* wave instructions per input */
-    constexpr u32 MAXI = (KMAX * PER + NW - 1) / NW;
-    const u32 ni = k * PER;
-    const uint8_t *bp[MAXI];
-#pragma unroll
-    for (u32 i = 0; i < MAXI; ++i) {
-        const u32 ins = wave + i * NW;
-        const u32 p = ins < ni ? ins / PER : k - 1;
-        bp[i] = base(p);
-    }
-    resolve_sgprs(bp);
-#pragma unroll
-    for (u32 i = 0; i < MAXI; ++i) {
-        const u32 ins = wave + i * NW;
-        if (ins >= ni)
-            break;
-        const u32 el = (ins % PER) * 64 + lane;  /* 16-B piece within input p */
-        const u32 seg = el >> 2;
-        const uint64_t slot = t0 + seg % T;
-        const uint64_t st = slot < nslots ? stripe(slot) : kNoSlot;
-        if (st != kNoSlot) {
-            const uint8_t *g = bp[i] + st * in_stride + (seg / T) * 64u + (el & 3u) * 16u;
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)g,
-                (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, LA);
-        }
-    }
-}
-
 /* wave-local LDS hand-off (the slice is private to the wave) */
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -975,20 +919,6 @@ struct PatWords {
                 w[lane] = v0;
                 w[lane + 64u] = v1;
             }
-        }
-    }
-    /* the (up to 4) words of src[]: byte p of them is input p's source */
-    __device__ __forceinline__ void src_words(const CombineArgs &a, u32 (&w)[4]) const
-    {
-        if constexpr (PG) {
-            w[0] = s0;
-            w[1] = s1;
-            w[2] = s2;
-            w[3] = s3;
-        } else {
-#pragma unroll
-            for (u32 i = 0; i < 4; ++i)
-                w[i] = i < a.kw ? a.pat[pb + i] : 0u;
         }
     }
     /* (the argument struct is passed in, not held: holding a reference to
