@@ -480,7 +480,11 @@ def heal_sweep(mode, windows=64):
                       patch's iobuf data allocator installs;
       ec_provenance_calloc  the same fragments, outputs from plain calloc (the
                       control: the patch without the data allocator, i.e. one
-                      call mixing mapped and pageable buffers).
+                      call mixing mapped and pageable buffers);
+      ec_provenance_rows  ec_provenance with the patch's ec_writev_encode,
+                      which codes only the bricks the heal write goes to
+                      (heal->bad = bricks 0..3: ec_method_encode_rows, 4 of
+                      12 fragments).
     Run in a child process per engine setting: `auto` (the crossover), `gpu`
     (EC_GPU_ALWAYS=1) and `cpu` (cpu-extensions=avx); the engine counters
     say where the calls went."""
@@ -496,7 +500,10 @@ def heal_sweep(mode, windows=64):
     mask = sum(1 << (r - 1) for r in rows)
     nwin = 4                                          # distinct windows, cycled
     res = {}
-    for prov in ("pageable", "registered", "ec_provenance", "ec_provenance_calloc"):
+    heal_rows = (1 << (n - k)) - 1                    # the lost bricks 0..3
+    for prov in ("pageable", "registered", "ec_provenance", "ec_provenance_calloc",
+                 "ec_provenance_rows"):
+        sel = heal_rows if prov == "ec_provenance_rows" else (1 << n) - 1
         keep, regs, pool = [], [], []
         ps0 = g.pool_stats()
         bufs = []
@@ -527,7 +534,7 @@ def heal_sweep(mode, windows=64):
             lib.ec_method_host_register_flush()
             for w in range(nwin):
                 frs = [pages[w * n + i][:fl] for i in range(n)]
-                if prov == "ec_provenance":
+                if prov in ("ec_provenance", "ec_provenance_rows"):
                     d = g.PoolBuffer(W + 64 + 4095)
                     e = g.PoolBuffer(n * fl + 64 + 4095)
                     pool += [d, e]
@@ -542,9 +549,15 @@ def heal_sweep(mode, windows=64):
             with g.ECMatrixList(k, n, gen="avx" if mode == "cpu" else "auto") as L:
                 for data, frs, out, eo in bufs:           # fragments to heal from
                     L.encode(W, data, frs)
+                def reencode(out, eo):
+                    if sel == (1 << n) - 1:
+                        L.encode(W, out, eo)
+                    else:
+                        L.encode_rows(W, out, sel, [e if (sel >> i) & 1 else None
+                                                    for i, e in enumerate(eo)])
                 data, frs, out, eo = bufs[0]              # warm (lazy setup)
                 L.decode(fl, mask, rows, [frs[r - 1] for r in rows], out)
-                L.encode(W, out, eo)
+                reencode(out, eo)
                 st0 = g.stats()
                 td, te = [], []
                 t0 = time.perf_counter()
@@ -553,13 +566,14 @@ def heal_sweep(mode, windows=64):
                     a = time.perf_counter()
                     L.decode(fl, mask, rows, [frs[r - 1] for r in rows], out)
                     b = time.perf_counter()
-                    L.encode(W, out, eo)
+                    reencode(out, eo)
                     te.append(time.perf_counter() - b)
                     td.append(b - a)
                 el = time.perf_counter() - t0
                 st1 = g.stats()
                 ok = all(np.array_equal(o, d) for d, _, o, _ in bufs) and all(
-                    np.array_equal(e[i], f[i]) for _, f, _, e in bufs for i in range(n))
+                    np.array_equal(e[i], f[i]) for _, f, _, e in bufs for i in range(n)
+                    if (sel >> i) & 1)
         finally:
             for p in regs:
                 lib.ec_method_host_unregister(p)
@@ -594,7 +608,9 @@ def heal_sweep_all(windows=256):
                provenances="pageable: plain malloc; registered: one registered region; "
                            "ec_provenance: the integration patch (fragments in deferred-registered "
                            "1 MiB-page arenas, outputs from the pinned pool); "
-                           "ec_provenance_calloc: registered fragments, calloc outputs")
+                           "ec_provenance_calloc: registered fragments, calloc outputs; "
+                           "ec_provenance_rows: ec_provenance with the patch's row-masked "
+                           "re-encode (ec_method_encode_rows, the 4 healed bricks only)")
     for mode in ("auto", "gpu", "cpu"):
         env = dict(os.environ)
         env.pop("EC_GPU_ALWAYS", None)

@@ -752,6 +752,28 @@ static bool zc_double_buffered()
     return v;
 }
 
+/* A/B knobs of the persistent zero-copy combine's grid (read once):
+ * EC_ZC_TPB = fixed tiles per block (r03's rule was 4), EC_ZC_INFLIGHT_KB =
+ * the input bytes one round of tiles keeps in flight (default 2048). */
+static uint64_t zc_env(const char *name, long lo, long hi, long dflt)
+{
+    const char *e = getenv(name);
+    const long v = e ? atol(e) : dflt;
+    return (uint64_t)(v >= lo && v <= hi ? v : dflt);
+}
+
+static uint64_t zc_fixed_tpb()
+{
+    static const uint64_t v = zc_env("EC_ZC_TPB", 1, 1024, 0);
+    return v;
+}
+
+static uint64_t zc_inflight_bytes()
+{
+    static const uint64_t v = zc_env("EC_ZC_INFLIGHT_KB", 64, 1 << 20, 2048) << 10;
+    return v;
+}
+
 /* CUs of the current device, queried once per device */
 static int cu_count()
 {
@@ -789,9 +811,17 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
     constexpr int NW = 8;
     const size_t lds_db = (size_t)(2 * d->k + d->rows) * 8 * ECD_CHUNK + 8 * ECD_MAX_ROWS;
     if (zc_double_buffered() && d->k <= 8 && lds_db <= (128u << 10) + 8 * ECD_MAX_ROWS) {
-        /* persistent, >= 4 tiles per block so its reads of tile i + 1 and
-         * writes of tile i overlap, at most one block per CU */
-        const uint64_t gdb = std::min<uint64_t>(std::max<uint64_t>(g / 4, 1), (uint64_t)cu_count());
+        /* persistent, at most one block per CU, >= 2 tiles per block so its
+         * reads of tile i + 1 and writes of tile i overlap, and as many
+         * blocks as keep ~2 MiB of input in flight: more only queue on the
+         * link, fewer leave it idle while each block's first tile lands.
+         * Pinned 8+4 / 4+2 calls, us (decode; profiles/r04/r04m_zctpb.log,
+         * r03's 4 tiles per block -> this): 8+4 1 MiB 81 -> 69, 4 MiB 173
+         * -> 164, 16 MiB 516 -> 505; 4+2 16 MiB 533 -> 489. */
+        const uint64_t tpb = zc_fixed_tpb();
+        const uint64_t want =
+            tpb ? g / tpb : std::min<uint64_t>(g / 2, zc_inflight_bytes() / ((uint64_t)d->k * 8 * ECD_CHUNK));
+        const uint64_t gdb = std::min<uint64_t>(std::max<uint64_t>(want, 1), (uint64_t)cu_count());
         const void *kern = d->k <= 4 ? (a.group_pattern ? (const void *)ec_combine_zc_db<4, NW, true>
                                                         : (const void *)ec_combine_zc_db<4, NW, false>)
                                      : (a.group_pattern ? (const void *)ec_combine_zc_db<8, NW, true>

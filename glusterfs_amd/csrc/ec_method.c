@@ -1298,6 +1298,148 @@ ec_method_encode_batch(ec_matrix_list_t *list, uint64_t nstripes, const void *in
     return encode_any(list, nstripes, in, out);
 }
 
+/* ------------------------------------------- encode of selected fragments */
+
+/* The encode-matrix rows of the bricks in row_mask (ec_method_matrix_normal,
+ * ec-method.c:22-36) as a k -> m combination of the stripe's data chunks;
+ * outs[] = the selected out[] entries in brick order. */
+static int
+rows_pattern(const ecm_ctx_t *ctx, uintptr_t row_mask, void *const *out, uint8_t *pat,
+             void **outs, uint32_t *m)
+{
+    uint32_t coef[ECM_MAX_N * ECM_MAX_K];
+    uint8_t src[ECM_MAX_K];
+    uint32_t i, p, t = 0;
+
+    if (row_mask == 0 || (row_mask >> ctx->n) != 0)
+        return -EINVAL;
+    for (i = 0; i < ctx->n; i++) {
+        if (!((row_mask >> i) & 1))
+            continue;
+        if (!out[i])
+            return -EINVAL;
+        for (p = 0; p < ctx->k; p++)
+            coef[t * ctx->k + p] = ctx->enc[i * ctx->k + p];
+        outs[t++] = out[i];
+    }
+    for (p = 0; p < ctx->k; p++)
+        src[p] = (uint8_t)p;
+    pack_pattern(pat, ctx->k, src, t, coef);
+    *m = t;
+    return 0;
+}
+
+/* Host buffers: the GPU pipeline's generic encode (the zero-copy combine with
+ * the selected rows as its pattern) or the CPU engine's combination.  Routed
+ * with the model and observations of a k -> m combination (a heal moves the
+ * same bytes) and not recorded: its rate per user byte is neither an
+ * encode's nor a full decode's, and exploration calls that never record
+ * would recur forever. */
+static int
+host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
+                 void *const *outs, const uint8_t *pat)
+{
+    const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE, user = fl * ctx->k;
+    const uint64_t bytes = fl * (ctx->k + m);
+    const struct enc_bufs eb = {in, outs, ctx->k, m, fl};
+    ecd_combine_desc_t d;
+    uint32_t p;
+    int rc;
+
+    if (!route_cpu(ctx, user, bytes, ECM_DECODE, 0) &&
+        !route_cpu(ctx, user, bytes, ECM_DECODE, enc_staged(&eb))) {
+        rc = ecd_encode_host(0, ctx->k, m, nstripes, in, outs, pat);
+        if (!gpu_failed(rc)) {
+            if (rc == 0)
+                stat_add(ECM_STAT_GPU);
+            return rc;
+        }
+    }
+    memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
+    d.k = ctx->k;
+    d.rows = m;
+    d.nstripes = nstripes;
+    d.in_stride = (uint64_t)ctx->k * EC_METHOD_CHUNK_SIZE;
+    d.out_stride = EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < ctx->k; p++)
+        d.in_base[p] = (const uint8_t *)in + (uint64_t)p * EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < m; p++)
+        d.out_base[p] = outs[p];
+    d.npatterns = 1;
+    d.pat_bytes = ctx->k + m * ctx->k;
+    d.pat_ext = pat;
+    rc = ecc_combine(ctx->isa, &d);
+    if (rc == 0)
+        stat_add(ECM_STAT_CPU);
+    return rc;
+}
+
+static int
+encode_rows_any(ec_matrix_list_t *list, uint64_t nstripes, const void *in, uintptr_t row_mask,
+                void *const *out)
+{
+    ecm_ctx_t *ctx = CTX(list);
+    uint8_t pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K];
+    void *outs[ECM_MAX_N];
+    ecd_combine_desc_t d;
+    uint32_t m = 0, p;
+    int dev, rc;
+
+    rc = rows_pattern(ctx, row_mask, out, pat, outs, &m);
+    if (rc || nstripes == 0)
+        return rc;
+    dev = ecd_ptr_device(in);
+    if (!bufs_on((const void *const *)outs, m, dev))
+        return -EINVAL; /* mixed host/device buffers are not supported */
+    if (dev < 0)
+        return host_encode_rows(ctx, nstripes, in, m, outs, pat);
+    memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
+    d.k = ctx->k;
+    d.rows = m;
+    d.nstripes = nstripes;
+    d.in_stride = (uint64_t)ctx->k * EC_METHOD_CHUNK_SIZE;
+    d.out_stride = EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < ctx->k; p++)
+        d.in_base[p] = (const uint8_t *)in + (uint64_t)p * EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < m; p++)
+        d.out_base[p] = outs[p];
+    d.npatterns = 1;
+    d.pat_bytes = ctx->k + m * ctx->k;
+    memcpy(d.pat, pat, d.pat_bytes);
+    rc = ecd_combine(dev, NULL, &d);
+    return rc ? rc : ecd_sync(dev, NULL);
+}
+
+void
+ec_method_encode_rows(ec_matrix_list_t *list, uint64_t size, void *in, uintptr_t row_mask,
+                      void **out)
+{
+    ecm_ctx_t *ctx = CTX(list);
+    uint32_t i;
+    int rc;
+
+    if (ctx && row_mask == ((uintptr_t)1 << ctx->n) - 1) {
+        ec_method_encode(list, size, in, out);
+        return;
+    }
+    if (!ctx || size % list->stripe != 0 || !out) {
+        ecm_log("ec_method_encode_rows: size %llu is not a multiple of the stripe (%u)",
+                (unsigned long long)size, list->stripe);
+        abort();
+    }
+    if (row_mask == 0)
+        return; /* no fragment wanted */
+    rc = encode_rows_any(list, size / list->stripe, in, row_mask, out);
+    if (rc != 0) {
+        ecm_log("ec_method_encode_rows(mask 0x%llx) failed (%d): %s",
+                (unsigned long long)row_mask, rc, ecd_last_error());
+        abort(); /* as ec_method_encode: never return bad data */
+    }
+    for (i = 0; i < ctx->n; i++)
+        if ((row_mask >> i) & 1)
+            out[i] = (uint8_t *)out[i] + size / list->columns;
+}
+
 static int
 decode_any(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask, const uint32_t *rows,
            const void *const *in, void *out)

@@ -44,7 +44,7 @@ EXPORTS = (
     "ec_method_inject_device_faults", "ec_method_device_numa_node", "ec_method_copy_threads",
     "ec_method_host_register_async", "ec_method_host_register_flush", "ec_method_buffer_get",
     "ec_method_buffer_put", "ec_method_pool_stats", "ec_method_xover_route",
-    "ec_method_xover_observe", "ec_method_xover_reset",
+    "ec_method_xover_observe", "ec_method_xover_reset", "ec_method_encode_rows",
 )
 
 
@@ -135,6 +135,7 @@ def _load():
         "ec_method_fini": (None, [P]),
         "ec_method_update": (i32, [vp, P, ctypes.c_char_p]),
         "ec_method_encode": (None, [P, u64, vp, vp]),
+        "ec_method_encode_rows": (None, [P, u64, vp, up, vp]),
         "ec_method_decode": (i32, [P, u64, up, vp, vp, vp]),
         "ec_method_encode_batch": (i32, [P, u64, vp, vp]),
         "ec_method_decode_batch": (i32, [P, u64, up, vp, vp, vp]),
@@ -405,6 +406,13 @@ class ECMatrixList:
         """ec_method_encode: `out` is a list of n fragment buffers."""
         ptrs = _ptr_array(out)
         lib.ec_method_encode(ctypes.byref(self._list), size, addr(inp), ptrs)
+
+    def encode_rows(self, size, inp, row_mask, out):
+        """ec_method_encode_rows: `out` is a list of n fragment buffers (None
+        where the bit of row_mask is clear); only the bricks in row_mask are
+        computed."""
+        lib.ec_method_encode_rows(ctypes.byref(self._list), size, addr(inp), row_mask,
+                                  _ptr_array(out))
 
     def decode(self, size, mask, rows, inp, out):
         """ec_method_decode: size = bytes per fragment; rows = brick idx + 1."""

@@ -145,6 +145,20 @@ int32_t ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes,
                                uint64_t group_stripes, const uintptr_t *group_masks,
                                const void *const *frags, void *out);
 
+/* Encode of selected fragments: ec_method_encode restricted to the fragments
+ * whose bit i is set in row_mask (bit i = brick i, the numbering of decode
+ * masks).  A heal write goes to the bad bricks only (ec-heal.c:327-329:
+ * ec_writev with heal->bad) and a degraded write skips the bricks that are
+ * down, yet ec_writev_encode (ec-inode-write.c:2125-2138) computes all n
+ * fragments; this computes |row_mask| of them, i.e. writes m*size/k instead
+ * of n*size/k bytes and does m/n of the arithmetic.  out[] is indexed by
+ * brick as in ec_method_encode: out[i] is read and advanced by size/k only for
+ * the bits of row_mask (the others may be NULL and are left alone).  A full
+ * row_mask is ec_method_encode, an empty one a no-op.  Cannot fail on host buffers; invalid
+ * arguments abort with a diagnostic, as ec_method_encode. */
+void ec_method_encode_rows(ec_matrix_list_t *list, uint64_t size, void *in,
+                           uintptr_t row_mask, void **out);
+
 /* Fused heal: regenerate the fragments of the bricks
  * in `target_mask` straight from the k fragments in `mask`, without
  * materialising the decoded data: out[j] (nstripes*512 bytes) is the fragment

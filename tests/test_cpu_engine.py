@@ -224,3 +224,58 @@ def test_large_calls_stream_outputs(ec, oracle, gen):
         odd = raw[8:8 + data.size]               # misaligned: regular stores
         L.decode_batch(nst, 0x3C, rows, [want[r - 1] for r in rows], odd)
         assert np.array_equal(odd, data)
+
+
+@pytest.mark.parametrize("gen", GENS)
+@pytest.mark.parametrize("k,n", [(2, 3), (4, 6), (8, 12), (16, 20), (10, 13)])
+def test_encode_rows_matches_oracle(ec, oracle, gen, k, n):
+    """ec_method_encode_rows: only the bricks of row_mask are computed (the
+    heal write of ec-heal.c:327-329 goes to heal->bad only), equal to those
+    fragments of the oracle's full encode; the other buffers are untouched."""
+    _isa_ok(ec, gen)
+    rng = np.random.default_rng(k * 7 + n)
+    masks = {1, 1 << (n - 1), (1 << (n - 1)) - 1}
+    masks |= {int(m) for m in rng.integers(1, 1 << n, 6)}
+    masks.discard((1 << n) - 1)
+    nst = 9
+    data = rnd(CHUNK * k * nst, k * 31 + n)
+    want = oracle.encode(k, n, data)
+    with ec.ECMatrixList(k, n, gen=gen) as L:
+        for m in sorted(masks):
+            outs = [np.full(CHUNK * nst, 0x5A, np.uint8) for _ in range(n)]
+            arg = [outs[i] if (m >> i) & 1 else None for i in range(n)]
+            L.encode_rows(data.size, data, m, arg)
+            for i in range(n):
+                if (m >> i) & 1:
+                    assert np.array_equal(outs[i], want[i]), (gen, k, n, hex(m), i)
+                else:
+                    assert (outs[i] == 0x5A).all(), (gen, k, n, hex(m), i)
+
+
+def test_encode_rows_pointer_contract(ec, oracle):
+    """As ec_method_encode (ec-method.c:405), each selected out[i] advances by
+    size/k; unselected entries (NULL here) stay as they are; an empty mask is
+    a no-op and a full mask is ec_method_encode."""
+    import ctypes
+    k, n, nst = 4, 6, 3
+    data = rnd(CHUNK * k * nst, 5)
+    want = oracle.encode(k, n, data)
+    with ec.ECMatrixList(k, n) as L:
+        outs = [np.zeros(CHUNK * nst, np.uint8) for _ in range(n)]
+        m = 0b100110
+        arr = (ctypes.c_void_p * n)(*[o.ctypes.data if (m >> i) & 1 else None
+                                      for i, o in enumerate(outs)])
+        ec.ec_method.lib.ec_method_encode_rows(ctypes.byref(L._list), data.size,
+                                               data.ctypes.data, m, arr)
+        for i in range(n):
+            if (m >> i) & 1:
+                assert arr[i] == outs[i].ctypes.data + data.size // k
+                assert np.array_equal(outs[i], want[i])
+            else:
+                assert arr[i] is None
+        ec.ec_method.lib.ec_method_encode_rows(ctypes.byref(L._list), data.size,
+                                               data.ctypes.data, 0, arr)   # no-op
+        full = [np.zeros(CHUNK * nst, np.uint8) for _ in range(n)]
+        L.encode_rows(data.size, data, (1 << n) - 1, full)
+        for i in range(n):
+            assert np.array_equal(full[i], want[i])

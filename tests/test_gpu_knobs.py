@@ -8,7 +8,9 @@ instead of caching it; EC_MI355X_LDSNT=1 stages these small calls with the
 non-temporal LDS-DMA loads that the library uses above 256 MiB of input;
 EC_MI355X_ZCDB=0 runs host-buffer combines (k <= 8) through the one tile per
 block zero-copy kernel instead of the persistent double-buffered one (the
-default since r04; =1 forces it), each with host decode, heal and mixed calls.
+default since r04; =1 forces it), each with host encode, decode, heal and
+mixed calls; EC_ZC_TPB (fixed tiles per block) and EC_ZC_INFLIGHT_KB (input
+bytes in flight per round of tiles) size the persistent zero-copy grid.
 Each runs here in its own process through the C ABI, bit-exact against the
 oracle on device-resident encode, full / partial decode (ragged tiles
 included) and mixed decode.
@@ -74,6 +76,12 @@ for k, n in ((4, 6), (8, 12), (16, 20)):
         # host buffers (EC_GPU_ALWAYS=1: the zero-copy combine over staged
         # pinned slots), several tiles per block of the persistent kernel
         for nst in (5, 1031, 4100):
+            hdata = rb(512 * k * nst)
+            hf = [np.empty(512 * nst, np.uint8) for _ in range(n)]
+            L.encode_batch(nst, hdata, hf)
+            wantf = O.encode(k, n, hdata)
+            for i in range(n):
+                assert np.array_equal(hf[i], wantf[i]), ("host enc", k, n, nst, i)
             frags = [rb(512 * nst) for _ in range(n)]
             out = np.empty(512 * k * nst, np.uint8)
             for m in masks[:4]:
@@ -104,7 +112,8 @@ print("ok")
 """
 
 KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1"),
-         ("EC_MI355X_ZCDB", "0"), ("EC_MI355X_ZCDB", "1")]
+         ("EC_MI355X_ZCDB", "0"), ("EC_MI355X_ZCDB", "1"), ("EC_ZC_TPB", "1"), ("EC_ZC_TPB", "16"),
+         ("EC_ZC_INFLIGHT_KB", "64")]
 
 
 @pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])

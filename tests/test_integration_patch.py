@@ -1,12 +1,13 @@
 """The reference-side binding as a patch:
 integration/glusterfs-ec-mi355x.patch must apply cleanly (-p1) to the
 reference's xlators/cluster/ec/src/{Makefile.am, ec-method.h, ec-types.h,
-ec.c} and libglusterfs/src/{iobuf.c, glusterfs/iobuf.h, libglusterfs.sym},
+ec.c, ec-inode-write.c} and libglusterfs/src/{iobuf.c, glusterfs/iobuf.h, libglusterfs.sym},
 drop every coding-layer source from ec.la, link libec_mi355x, leave
 ec-method.h including the library header after ec-types.h, keep every
 header ec.c includes in the distributed header list, and register the
 client's iobuf arenas with the coder (pinned, device-mapped: zero copy)
-after their mmap and unregister them before their munmap.  Works on a
+after their mmap and unregister them before their munmap, and let a write
+code only the fragments of the bricks it goes to.  Works on a
 scratch copy; skipped where the reference tree is absent (the GPU box)."""
 import os
 import re
@@ -21,7 +22,7 @@ REF = "/root/reference"
 SUB = os.path.join("xlators", "cluster", "ec", "src")
 LIBSRC = os.path.join("libglusterfs", "src")
 FILES = tuple(os.path.join(SUB, f) for f in ("Makefile.am", "ec-method.h", "ec-types.h",
-                                             "ec.c")) + \
+                                             "ec.c", "ec-inode-write.c")) + \
     tuple(os.path.join(LIBSRC, f) for f in ("iobuf.c", os.path.join("glusterfs", "iobuf.h"),
                                            "libglusterfs.sym"))
 
@@ -156,3 +157,24 @@ def test_patched_iobuf_data_allocator_covers_every_size_class(scratch):
     # the free hook is kept when the last volume goes (buffers still out)
     assert "iobuf_set_data_allocator(this->ctx->iobuf_pool, NULL,\n" in put
     assert "ec_iobuf_data_free);" in put
+
+
+def test_patched_writev_encodes_only_target_bricks(scratch):
+    """ec_writev_encode (ec-inode-write.c:2125-2138) codes the fragments of the
+    bricks the write can be wound to: fop->mask (ec_child_select only clears
+    its bits) plus the healing bricks it adds back (the fop's and its
+    parent's), limited to the volume's nodes -- so a heal write
+    (ec-heal.c:327-329, heal->bad) computes only the bad bricks' fragments."""
+    subprocess.run(["patch", "-p1", "--batch", "-i", PATCH], cwd=scratch, check=True,
+                   capture_output=True)
+    src = (scratch / SUB / "ec-inode-write.c").read_text()
+    body = _c_body(src, "ec_writev_encode")
+    assert "ec_method_encode(" not in body
+    assert "targets = fop->mask | fop->healing;" in body
+    assert "targets |= fop->parent->healing;" in body
+    assert "targets & ec->node_mask" in body
+    assert "ec_method_encode_rows(&ec->matrix, fop->vector[0].iov_len," in body
+    # the dispatch that follows the encode is the one whose mask this bounds
+    mgr = _c_body(src, "ec_manager_writev")
+    e = mgr.index("ec_writev_encode(fop);")
+    assert mgr.index("ec_dispatch_all(fop);", e) - e < 80

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Host-buffer decode time per call by size (development probe, GPU box):
-8+4 and 4+2 decodes from pinned buffers (ec_method_host_alloc, i.e. the
-zero-copy combine) at 4-256 MiB of user data, median of repeated calls.
-Run once per EC_MI355X_ZCDB setting (read at library load); EC_GPU_ALWAYS=1
-keeps every call on the GPU.  Usage: python tools/zc_sizes.py"""
+8+4 and 4+2 decodes and encodes from pinned buffers (ec_method_host_alloc,
+i.e. the zero-copy kernels) at ZC_SIZES MiB of user data (default 4 16 64
+256), median of repeated calls.  Run once per knob setting (EC_MI355X_ZCDB,
+EC_ZC_TPB, EC_ZC_INFLIGHT_KB: read at library load); EC_GPU_ALWAYS=1 keeps every
+call on the GPU.  Usage: python tools/zc_sizes.py"""
 import ctypes
 import os
 import sys
@@ -26,16 +27,19 @@ def pinned(lib, nb):
 
 def main():
     lib = g.ec_method.lib
-    print("EC_MI355X_ZCDB=%s" % os.environ.get("EC_MI355X_ZCDB", "unset"))
+    knobs = " ".join("%s=%s" % (v, os.environ.get(v, "unset"))
+                     for v in ("EC_MI355X_ZCDB", "EC_ZC_TPB", "EC_ZC_INFLIGHT_KB"))
+    print(knobs)
+    sizes = [float(x) for x in os.environ.get("ZC_SIZES", "4 16 64 256").split()]
     for k, n in ((8, 12), (4, 6)):
-        for mib in (4, 16, 64, 256):
-            S = mib << 20
+        for mib in sizes:
+            S = int(mib * (1 << 20)) // (512 * k) * (512 * k)
             nst = S // (512 * k)
             bufs = []
             try:
                 din_p, din = pinned(lib, S)
                 bufs.append(din_p)
-                din[:] = np.random.default_rng(mib).integers(0, 256, S, dtype=np.uint8)
+                din[:] = np.random.default_rng(int(mib * 16)).integers(0, 256, S, dtype=np.uint8)
                 fr = [pinned(lib, nst * 512) for _ in range(n)]
                 bufs += [p for p, _ in fr]
                 dout_p, dout = pinned(lib, S)
@@ -53,10 +57,20 @@ def main():
                         L.decode_batch(nst, mask, rows, ins, dout_p)
                         ts.append(time.perf_counter() - t0)
                     ok = bool(np.array_equal(dout, din))
+                    te = []
+                    frs = [p for p, _ in fr]
+                    want = [a.copy() for _, a in fr]
+                    for _ in range(reps):
+                        t0 = time.perf_counter()
+                        L.encode_batch(nst, din_p, frs)
+                        te.append(time.perf_counter() - t0)
+                    ok = ok and all(np.array_equal(a, w) for (_, a), w in zip(fr, want))
                 ts.sort()
-                med = ts[len(ts) // 2]
-                print("%d+%d decode %4d MiB: %9.1f us per call, %6.2f GB/s user, ok %s"
-                      % (k, n - k, mib, med * 1e6, S / med / 1e9, ok))
+                te.sort()
+                med, mede = ts[len(ts) // 2], te[len(te) // 2]
+                print("%d+%d %7.2f MiB: decode %8.1f us %6.2f GB/s, encode %8.1f us %6.2f GB/s,"
+                      " ok %s [%s]" % (k, n - k, mib, med * 1e6, S / med / 1e9, mede * 1e6,
+                                       S / mede / 1e9, ok, knobs))
             finally:
                 for p in bufs:
                     lib.ec_method_host_free(p)
