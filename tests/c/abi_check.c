@@ -1,7 +1,8 @@
 /* Compiled with plain gcc against include/ec_method.h and linked against
  * glusterfs_amd/lib/libec_mi355x.so, the way GlusterFS's ec xlator would
  * (INTEGRATION.md).  Checks the 120-byte ec_matrix_list_t layout of
- * ec-types.h:549-562 and exercises ec_method_init/encode/decode/fini:
+ * ec-types.h:549-562 and exercises ec_method_init/encode/decode/fini and the
+ * row-masked encode the integration patch's ec_writev_encode calls:
  * argv[1] = "gpu" requires the gfx950 engine, "cpu" the CPU engine (a node
  * without GPU, or cpu-extensions=none). */
 #include <errno.h>
@@ -65,6 +66,20 @@ main(int argc, char **argv)
         if (rc != 0 || memcmp(in, dec, 512 * K * NST) != 0) {
             printf("decode rc=%d mismatch\n", rc);
             return 6;
+        }
+        {
+            /* a heal write of bricks 0 and 1 (the patch's ec_writev_encode):
+             * only those two fragments, equal to the full encode's */
+            unsigned char *h0 = malloc(512 * NST), *h1 = malloc(512 * NST);
+            void *hs[N] = {h0, h1, NULL, NULL, NULL, NULL};
+            ec_method_encode_rows(&list, 512 * K * NST, in, 0x3, hs);
+            if (hs[0] != h0 + 512 * NST || hs[2] != NULL ||
+                memcmp(h0, frag[0], 512 * NST) != 0 || memcmp(h1, frag[1], 512 * NST) != 0) {
+                printf("encode_rows mismatch\n");
+                return 8;
+            }
+            free(h0);
+            free(h1);
         }
         printf("roundtrip ok\n");
     }
