@@ -484,7 +484,11 @@ def heal_sweep(mode, windows=64):
       ec_provenance_rows  ec_provenance with the patch's ec_writev_encode,
                       which codes only the bricks the heal write goes to
                       (heal->bad = bricks 0..3: ec_method_encode_rows, 4 of
-                      12 fragments).
+                      12 fragments);
+      ec_provenance_fused  the same buffers through the fused heal
+                      (ec_method_heal: the 4 bad bricks' fragments straight
+                      from the 8 good ones, no decoded window) -- what a heal
+                      that read raw fragments would run.
     Run in a child process per engine setting: `auto` (the crossover), `gpu`
     (EC_GPU_ALWAYS=1) and `cpu` (cpu-extensions=avx); the engine counters
     say where the calls went."""
@@ -502,8 +506,9 @@ def heal_sweep(mode, windows=64):
     res = {}
     heal_rows = (1 << (n - k)) - 1                    # the lost bricks 0..3
     for prov in ("pageable", "registered", "ec_provenance", "ec_provenance_calloc",
-                 "ec_provenance_rows"):
-        sel = heal_rows if prov == "ec_provenance_rows" else (1 << n) - 1
+                 "ec_provenance_rows", "ec_provenance_fused"):
+        sel = heal_rows if prov in ("ec_provenance_rows", "ec_provenance_fused") else (1 << n) - 1
+        fused = prov == "ec_provenance_fused"
         keep, regs, pool = [], [], []
         ps0 = g.pool_stats()
         bufs = []
@@ -534,7 +539,7 @@ def heal_sweep(mode, windows=64):
             lib.ec_method_host_register_flush()
             for w in range(nwin):
                 frs = [pages[w * n + i][:fl] for i in range(n)]
-                if prov in ("ec_provenance", "ec_provenance_rows"):
+                if prov in ("ec_provenance", "ec_provenance_rows", "ec_provenance_fused"):
                     d = g.PoolBuffer(W + 64 + 4095)
                     e = g.PoolBuffer(n * fl + 64 + 4095)
                     pool += [d, e]
@@ -555,23 +560,30 @@ def heal_sweep(mode, windows=64):
                     else:
                         L.encode_rows(W, out, sel, [e if (sel >> i) & 1 else None
                                                     for i, e in enumerate(eo)])
+                def heal_window(frs, out, eo):
+                    if fused:
+                        L.heal(nst, mask, [frs[r - 1] for r in rows], sel,
+                               [e for i, e in enumerate(eo) if (sel >> i) & 1])
+                        return time.perf_counter()
+                    L.decode(fl, mask, rows, [frs[r - 1] for r in rows], out)
+                    b = time.perf_counter()
+                    reencode(out, eo)
+                    return b
+
                 data, frs, out, eo = bufs[0]              # warm (lazy setup)
-                L.decode(fl, mask, rows, [frs[r - 1] for r in rows], out)
-                reencode(out, eo)
+                heal_window(frs, out, eo)
                 st0 = g.stats()
                 td, te = [], []
                 t0 = time.perf_counter()
                 for i in range(windows):
                     data, frs, out, eo = bufs[i % nwin]
                     a = time.perf_counter()
-                    L.decode(fl, mask, rows, [frs[r - 1] for r in rows], out)
-                    b = time.perf_counter()
-                    reencode(out, eo)
+                    b = heal_window(frs, out, eo)
                     te.append(time.perf_counter() - b)
                     td.append(b - a)
                 el = time.perf_counter() - t0
                 st1 = g.stats()
-                ok = all(np.array_equal(o, d) for d, _, o, _ in bufs) and all(
+                ok = (fused or all(np.array_equal(o, d) for d, _, o, _ in bufs)) and all(
                     np.array_equal(e[i], f[i]) for _, f, _, e in bufs for i in range(n)
                     if (sel >> i) & 1)
         finally:
@@ -610,7 +622,9 @@ def heal_sweep_all(windows=256):
                            "1 MiB-page arenas, outputs from the pinned pool); "
                            "ec_provenance_calloc: registered fragments, calloc outputs; "
                            "ec_provenance_rows: ec_provenance with the patch's row-masked "
-                           "re-encode (ec_method_encode_rows, the 4 healed bricks only)")
+                           "re-encode (ec_method_encode_rows, the 4 healed bricks only); "
+                           "ec_provenance_fused: ec_method_heal on the same buffers "
+                           "(decode_us_median = the whole heal call, encode 0)")
     for mode in ("auto", "gpu", "cpu"):
         env = dict(os.environ)
         env.pop("EC_GPU_ALWAYS", None)

@@ -1422,9 +1422,9 @@ ec_method_encode_rows(ec_matrix_list_t *list, uint64_t size, void *in, uintptr_t
         ec_method_encode(list, size, in, out);
         return;
     }
-    if (!ctx || size % list->stripe != 0 || !out) {
-        ecm_log("ec_method_encode_rows: size %llu is not a multiple of the stripe (%u)",
-                (unsigned long long)size, list->stripe);
+    if (!ctx || size % list->stripe != 0 || !out || (!in && size)) {
+        ecm_log("ec_method_encode_rows: bad arguments (size %llu, stripe %u, in %p, out %p)",
+                (unsigned long long)size, list->stripe, in, (void *)out);
         abort();
     }
     if (row_mask == 0)
