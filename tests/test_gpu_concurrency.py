@@ -57,13 +57,18 @@ def host_buf(ec, kind, nbytes, keep):
         p = ec.PinnedArray(nbytes + 8)
         keep.append(p)
         return p.array[8:]
+    if kind == "pool":            # the integration patch's iobuf memory
+        p = ec.PoolBuffer(nbytes)
+        keep.append(p)
+        return p.array[:nbytes]
     return np.empty(nbytes, np.uint8)
 
 
-@pytest.mark.parametrize("kind", ["pageable", "pinned", "misaligned"])
+@pytest.mark.parametrize("kind", ["pageable", "pinned", "misaligned", "pool"])
 def test_concurrent_mixed_geometries(ec, oracle, kind):
-    """16 threads on 4 volumes: encode, decode with a random mask and heal,
-    random sizes from 1 stripe to just under the queue limit."""
+    """16 threads on 4 volumes: encode, decode with a random mask, heal and a
+    row-masked encode (a heal write), random sizes from 1 stripe to just
+    under the queue limit."""
     geoms = [(4, 6), (8, 12), (16, 20), (5, 7)]
     lists = {g: ec.ECMatrixList(*g) for g in geoms}
     keep = []
@@ -95,6 +100,13 @@ def test_concurrent_mixed_geometries(ec, oracle, kind):
             L.heal(nst, mask, [frags[r - 1] for r in rows], sum(1 << b for b in lost), outs)
             for o, b in zip(outs, lost):
                 assert np.array_equal(o, want[b]), (t, it, "heal", b)
+            sel = int(rng.integers(1, (1 << n) - 1))
+            hw = [host_buf(ec, kind, CHUNK * nst, keep) if (sel >> i) & 1 else None
+                  for i in range(n)]
+            L.encode_rows(data.size, src, sel, hw)
+            for i, o in enumerate(hw):
+                if o is not None:
+                    assert np.array_equal(o, want[i]), (t, it, "encode_rows", hex(sel), i)
 
     try:
         run_threads(worker, 16)
