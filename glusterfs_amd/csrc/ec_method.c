@@ -1374,25 +1374,14 @@ host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
     return rc;
 }
 
+/* the k -> m combination of encode_rows on device buffers, queued on stream */
 static int
-encode_rows_any(ec_matrix_list_t *list, uint64_t nstripes, const void *in, uintptr_t row_mask,
-                void *const *out)
+device_encode_rows(ecm_ctx_t *ctx, int dev, void *stream, uint64_t nstripes, const void *in,
+                   uint32_t m, void *const *outs, const uint8_t *pat)
 {
-    ecm_ctx_t *ctx = CTX(list);
-    uint8_t pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K];
-    void *outs[ECM_MAX_N];
     ecd_combine_desc_t d;
-    uint32_t m = 0, p;
-    int dev, rc;
+    uint32_t p;
 
-    rc = rows_pattern(ctx, row_mask, out, pat, outs, &m);
-    if (rc || nstripes == 0)
-        return rc;
-    dev = ecd_ptr_device(in);
-    if (!bufs_on((const void *const *)outs, m, dev))
-        return -EINVAL; /* mixed host/device buffers are not supported */
-    if (dev < 0)
-        return host_encode_rows(ctx, nstripes, in, m, outs, pat);
     memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
     d.k = ctx->k;
     d.rows = m;
@@ -1406,8 +1395,49 @@ encode_rows_any(ec_matrix_list_t *list, uint64_t nstripes, const void *in, uintp
     d.npatterns = 1;
     d.pat_bytes = ctx->k + m * ctx->k;
     memcpy(d.pat, pat, d.pat_bytes);
-    rc = ecd_combine(dev, NULL, &d);
+    return ecd_combine(dev, stream, &d);
+}
+
+static int
+encode_rows_any(ec_matrix_list_t *list, uint64_t nstripes, const void *in, uintptr_t row_mask,
+                void *const *out)
+{
+    ecm_ctx_t *ctx = CTX(list);
+    uint8_t pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K];
+    void *outs[ECM_MAX_N];
+    uint32_t m = 0;
+    int dev, rc;
+
+    rc = rows_pattern(ctx, row_mask, out, pat, outs, &m);
+    if (rc || nstripes == 0)
+        return rc;
+    dev = ecd_ptr_device(in);
+    if (!bufs_on((const void *const *)outs, m, dev))
+        return -EINVAL; /* mixed host/device buffers are not supported */
+    if (dev < 0)
+        return host_encode_rows(ctx, nstripes, in, m, outs, pat);
+    rc = device_encode_rows(ctx, dev, NULL, nstripes, in, m, outs, pat);
     return rc ? rc : ecd_sync(dev, NULL);
+}
+
+int32_t
+ec_method_encode_rows_device(ec_matrix_list_t *list, int device, void *stream,
+                             uint64_t nstripes, const void *in, uintptr_t row_mask,
+                             void *const *out)
+{
+    uint8_t pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K];
+    void *outs[ECM_MAX_N];
+    uint32_t m = 0;
+    int rc;
+
+    if (!list || !CTX(list) || !out || (!in && nstripes))
+        return -EINVAL;
+    if (row_mask == 0 || nstripes == 0)
+        return (row_mask >> CTX(list)->n) ? -EINVAL : 0;
+    rc = rows_pattern(CTX(list), row_mask, out, pat, outs, &m);
+    if (rc)
+        return rc;
+    return device_encode_rows(CTX(list), device, stream, nstripes, in, m, outs, pat);
 }
 
 void

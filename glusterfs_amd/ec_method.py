@@ -45,6 +45,7 @@ EXPORTS = (
     "ec_method_host_register_async", "ec_method_host_register_flush", "ec_method_buffer_get",
     "ec_method_buffer_put", "ec_method_pool_stats", "ec_method_xover_route",
     "ec_method_xover_observe", "ec_method_xover_reset", "ec_method_encode_rows",
+    "ec_method_encode_rows_device",
 )
 
 
@@ -136,6 +137,7 @@ def _load():
         "ec_method_update": (i32, [vp, P, ctypes.c_char_p]),
         "ec_method_encode": (None, [P, u64, vp, vp]),
         "ec_method_encode_rows": (None, [P, u64, vp, up, vp]),
+        "ec_method_encode_rows_device": (i32, [P, ctypes.c_int, vp, u64, vp, up, vp]),
         "ec_method_decode": (i32, [P, u64, up, vp, vp, vp]),
         "ec_method_encode_batch": (i32, [P, u64, vp, vp]),
         "ec_method_decode_batch": (i32, [P, u64, up, vp, vp, vp]),
@@ -458,6 +460,14 @@ class ECMatrixList:
                       "ec_method_heal")
 
     # --- device-resident, asynchronous --------------------------------------
+    def encode_rows_device(self, device, stream, nstripes, inp, row_mask, out):
+        """ec_method_encode_rows_device: out[i] (None where the bit of
+        row_mask is clear) on device `device`, queued on `stream`."""
+        return _check(lib.ec_method_encode_rows_device(ctypes.byref(self._list), device, stream,
+                                                       nstripes, addr(inp), row_mask,
+                                                       _ptr_array(out)),
+                      "ec_method_encode_rows_device")
+
     def encode_device(self, device, stream, nstripes, inp, out):
         return _check(lib.ec_method_encode_device(ctypes.byref(self._list), device, stream,
                                                   nstripes, addr(inp), _ptr_array(out)),

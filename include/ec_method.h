@@ -214,6 +214,11 @@ int32_t ec_method_heal_device(ec_matrix_list_t *list, int device, void *stream,
                               uint64_t nstripes, uintptr_t mask,
                               const void *const *in, uintptr_t target_mask,
                               void *const *out);
+/* ec_method_encode_rows on device buffers: out[i] (indexed by brick) is
+ * written for the bits of row_mask only; out[] is not modified. */
+int32_t ec_method_encode_rows_device(ec_matrix_list_t *list, int device, void *stream,
+                                     uint64_t nstripes, const void *in, uintptr_t row_mask,
+                                     void *const *out);
 int32_t ec_method_writev_encode_device(ec_matrix_list_t *list, int device, void *stream,
                                        uint64_t head, uint64_t size, const void *user,
                                        const void *old_head, const void *old_tail,

@@ -105,3 +105,31 @@ def test_encode_rows_device(oracle, k, n):
                     assert np.array_equal(got, want[i]), (k, n, hex(m), i)
                 else:
                     assert (got == 0x5A).all()
+
+
+@pytest.mark.parametrize("k,n", GEOS)
+def test_encode_rows_device_async(oracle, k, n):
+    """ec_method_encode_rows_device on a side stream, then synchronised."""
+    import torch
+    import glusterfs_amd as g
+    nst = 777
+    data = rnd(CHUNK * k * nst, 5 * k)
+    want = oracle.encode(k, n, data)
+    din = torch.from_numpy(data).cuda()
+    st = torch.cuda.Stream()
+    with g.ECMatrixList(k, n) as L:
+        m = masks_for(n)[-1]
+        outs = [torch.full((CHUNK * nst,), 0x5A, dtype=torch.uint8, device="cuda")
+                for _ in range(n)]
+        torch.cuda.synchronize()
+        L.encode_rows_device(0, st.cuda_stream, nst, din, m,
+                             [o if (m >> i) & 1 else None for i, o in enumerate(outs)])
+        st.synchronize()
+        for i in range(n):
+            got = outs[i].cpu().numpy()
+            if (m >> i) & 1:
+                assert np.array_equal(got, want[i]), (k, n, hex(m), i)
+            else:
+                assert (got == 0x5A).all()
+        with pytest.raises(OSError):
+            L.encode_rows_device(0, st.cuda_stream, nst, din, 1 << n, outs)
