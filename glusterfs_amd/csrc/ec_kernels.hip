@@ -752,6 +752,9 @@ static bool zc_double_buffered()
     return v;
 }
 
+/* LDS of one gfx950 CU (MI355X_MICROARCH.md): the largest block LDS */
+constexpr size_t kLdsPerCu = 160u << 10;
+
 /* A/B knobs of the persistent zero-copy combine's grid (read once):
  * EC_ZC_TPB = fixed tiles per block (r03's rule was 4), EC_ZC_INFLIGHT_KB =
  * the input bytes one round of tiles keeps in flight (default 2048). */
@@ -810,7 +813,9 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
     const size_t lds = (size_t)(d->k + d->rows) * 8 * ECD_CHUNK;
     constexpr int NW = 8;
     const size_t lds_db = (size_t)(2 * d->k + d->rows) * 8 * ECD_CHUNK + 8 * ECD_MAX_ROWS;
-    if (zc_double_buffered() && d->k <= 8 && lds_db <= (128u << 10) + 8 * ECD_MAX_ROWS) {
+    const bool db16 = d->k > 8 && lds_db <= kLdsPerCu;   /* 16+4 heal / row-masked encode */
+    if (zc_double_buffered() &&
+        ((d->k <= 8 && lds_db <= (128u << 10) + 8 * ECD_MAX_ROWS) || db16)) {
         /* persistent, at most one block per CU, >= 2 tiles per block so its
          * reads of tile i + 1 and writes of tile i overlap, and as many
          * blocks as keep ~2 MiB of input in flight: more only queue on the
@@ -822,11 +827,15 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
         const uint64_t want =
             tpb ? g / tpb : std::min<uint64_t>(g / 2, zc_inflight_bytes() / ((uint64_t)d->k * 8 * ECD_CHUNK));
         const uint64_t gdb = std::min<uint64_t>(std::max<uint64_t>(want, 1), (uint64_t)cu_count());
-        const void *kern = d->k <= 4 ? (a.group_pattern ? (const void *)ec_combine_zc_db<4, NW, true>
-                                                        : (const void *)ec_combine_zc_db<4, NW, false>)
-                                     : (a.group_pattern ? (const void *)ec_combine_zc_db<8, NW, true>
-                                                        : (const void *)ec_combine_zc_db<8, NW, false>);
-        if (lds_db > (64u << 10) && ensure_lds_limit(kern, (int)((128u << 10) + 8 * ECD_MAX_ROWS)) != 0)
+        const void *kern =
+            db16 ? (a.group_pattern ? (const void *)ec_combine_zc_db<16, NW, true>
+                                    : (const void *)ec_combine_zc_db<16, NW, false>)
+            : d->k <= 4 ? (a.group_pattern ? (const void *)ec_combine_zc_db<4, NW, true>
+                                           : (const void *)ec_combine_zc_db<4, NW, false>)
+                        : (a.group_pattern ? (const void *)ec_combine_zc_db<8, NW, true>
+                                           : (const void *)ec_combine_zc_db<8, NW, false>);
+        if (lds_db > (64u << 10) &&
+            ensure_lds_limit(kern, db16 ? (int)kLdsPerCu : (int)((128u << 10) + 8 * ECD_MAX_ROWS)) != 0)
             return -EIO;
         void *args[] = {&a};
         if (hipLaunchKernel(kern, dim3((u32)gdb), dim3(NW * 64), args, lds_db, s) != hipSuccess)

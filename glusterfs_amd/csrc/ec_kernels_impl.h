@@ -1412,7 +1412,9 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
  * vmcnt(0) per barrier, which is wanted only at the end of an iteration).
  * The row bases live in LDS: a lane-indexed out_base[r] is a vector load
  * from the kernel arguments, whose vmcnt(0) would wait for the staging too.
- * LDS = (2k + rows) * 4 KiB + 8 * ECD_MAX_ROWS. */
+ * LDS = (2k + rows) * 4 KiB + 8 * ECD_MAX_ROWS: k <= 8 any rows up to 16,
+ * k = 16 (r04) up to 7 rows in the CU's 160 KiB -- the heal and the
+ * row-masked encode of a 16+4 volume, not its 16-row decode. */
 __device__ __forceinline__ uint64_t lds_read_u64(const uint8_t *p)
 {
     uint64_t v;
@@ -1492,15 +1494,21 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
                 const u32 rw = a.kw * (1 + r);
                 const u32 w0 = pw.word(a, rw);
                 const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
+                const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
+                const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
                 u32 acc[8][2], y[8][2];
 #pragma unroll
                 for (int b = 0; b < 8; ++b)
                     acc[b][0] = acc[b][1] = 0;
+                /* one coefficient byte per input, shifted out of a 64-bit
+                 * (K <= 8) or 128-bit (K = 16) scalar register pair */
                 uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
+                uint64_t ch = (uint64_t)w2 | ((uint64_t)w3 << 32);
 #pragma unroll 1
                 for (u32 p = 0; p < k; ++p) {
                     const u32 c = __builtin_amdgcn_readfirstlane((u32)cl & 0xFFu);
-                    cl >>= 8;
+                    cl = (cl >> 8) | (ch << 56);
+                    ch >>= 8;
                     if (c == 0)          /* ec-code-c.c:11666-11676 */
                         continue;
                     const uint8_t *src = col + p * (T * ECD_CHUNK);

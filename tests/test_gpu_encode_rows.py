@@ -3,7 +3,8 @@ only (a heal write goes to heal->bad only, ec-heal.c:327-329, yet
 ec_writev_encode computes all n, ec-inode-write.c:2125-2138).  Host buffers
 (EC_GPU_ALWAYS=1, tests/conftest.py) run the device layer's generic encode:
 the persistent zero-copy combine with the selected encode-matrix rows as its
-pattern (k <= 8) or ec_combine_zc (k = 16), read in place when pinned and
+pattern (k = 16 too while 2k + m tiles fit the CU's 160 KiB of LDS, i.e. up
+to 7 rows), read in place when pinned and
 through the staging slots when pageable; device buffers run ec_combine.  Every
 case is compared bit for bit with the oracle's full encode (the checker)."""
 import ctypes
@@ -45,7 +46,9 @@ def test_encode_rows_host_pageable(oracle, k, n):
                         assert np.array_equal(outs[i], want[i]), (k, n, nst, hex(m), i)
                     else:
                         assert (outs[i] == 0x5A).all()
-    assert g.ec_method.stats()["gpu_calls"] > s0["gpu_calls"]
+    s1 = g.ec_method.stats()
+    assert s1["gpu_calls"] > s0["gpu_calls"]
+    assert s1["cpu_fallbacks"] == s0["cpu_fallbacks"]   # no device error redone on the CPU
 
 
 @pytest.mark.parametrize("k,n", GEOS)
@@ -64,6 +67,7 @@ def test_encode_rows_host_pinned(oracle, k, n):
         ptrs.append(p)
         return p, np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(p))
 
+    s0 = g.ec_method.stats()
     try:
         ip, ia = pinned(S)
         ia[:] = rnd(S, 77)
@@ -83,6 +87,7 @@ def test_encode_rows_host_pinned(oracle, k, n):
     finally:
         for p in ptrs:
             lib.ec_method_host_free(p)
+    assert g.ec_method.stats()["cpu_fallbacks"] == s0["cpu_fallbacks"]
 
 
 @pytest.mark.parametrize("k,n", GEOS)

@@ -108,6 +108,7 @@ for k, n in ((4, 6), (8, 12), (16, 20)):
                 a0, a1 = gi * grp * 512, min(nst, (gi + 1) * grp) * 512
                 exp = O.decode(k, rws, [frags[r - 1][a0:a1] for r in rws])
                 assert np.array_equal(out[a0 * k:a1 * k], exp), ("host mixed", k, n, nst, gi)
+assert g.ec_method.stats()["cpu_fallbacks"] == 0   # every host call ran on the GPU
 print("ok")
 """
 

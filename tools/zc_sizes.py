@@ -31,7 +31,10 @@ def main():
                      for v in ("EC_MI355X_ZCDB", "EC_ZC_TPB", "EC_ZC_INFLIGHT_KB"))
     print(knobs)
     sizes = [float(x) for x in os.environ.get("ZC_SIZES", "4 16 64 256").split()]
-    for k, n in ((8, 12), (4, 6)):
+    geos = [tuple(int(x) for x in gk.split("+")) for gk in
+            os.environ.get("ZC_GEOS", "8+4 4+2").split()]
+    for k, r in geos:
+        n = k + r
         for mib in sizes:
             S = int(mib * (1 << 20)) // (512 * k) * (512 * k)
             nst = S // (512 * k)
@@ -65,12 +68,39 @@ def main():
                         L.encode_batch(nst, din_p, frs)
                         te.append(time.perf_counter() - t0)
                     ok = ok and all(np.array_equal(a, w) for (_, a), w in zip(fr, want))
+                    # heal of the n - k bricks outside `rows` (fragments in,
+                    # their fragments out) and the row-masked re-encode of a
+                    # heal write to them (user data in, their fragments out)
+                    lost = [b for b in range(n) if not (mask >> b) & 1]
+                    hp = [pinned(lib, nst * 512) for _ in lost]
+                    bufs += [p for p, _ in hp]
+                    th, tr = [], []
+                    for _ in range(reps):
+                        t0 = time.perf_counter()
+                        L.heal(nst, mask, ins, sum(1 << b for b in lost), [p for p, _ in hp])
+                        th.append(time.perf_counter() - t0)
+                    ok = ok and all(np.array_equal(a, want[b]) for (_, a), b in zip(hp, lost))
+                    sel = sum(1 << b for b in lost)
+                    arg = [None] * n
+                    for (p, _), b in zip(hp, lost):
+                        arg[b] = p
+                    for (_, a) in hp:
+                        a[:] = 0
+                    for _ in range(reps):
+                        t0 = time.perf_counter()
+                        L.encode_rows(S, din_p, sel, list(arg))
+                        tr.append(time.perf_counter() - t0)
+                    ok = ok and all(np.array_equal(a, want[b]) for (_, a), b in zip(hp, lost))
                 ts.sort()
                 te.sort()
+                th.sort()
+                tr.sort()
                 med, mede = ts[len(ts) // 2], te[len(te) // 2]
+                medh, medr = th[len(th) // 2], tr[len(tr) // 2]
                 print("%d+%d %7.2f MiB: decode %8.1f us %6.2f GB/s, encode %8.1f us %6.2f GB/s,"
-                      " ok %s [%s]" % (k, n - k, mib, med * 1e6, S / med / 1e9, mede * 1e6,
-                                       S / mede / 1e9, ok, knobs))
+                      " heal %8.1f us, encode_rows %8.1f us, ok %s [%s]"
+                      % (k, n - k, mib, med * 1e6, S / med / 1e9, mede * 1e6, S / mede / 1e9,
+                         medh * 1e6, medr * 1e6, ok, knobs))
             finally:
                 for p in bufs:
                     lib.ec_method_host_free(p)
