@@ -814,6 +814,30 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
     constexpr int NW = 8;
     const size_t lds_db = (size_t)(2 * d->k + d->rows) * 8 * ECD_CHUNK + 8 * ECD_MAX_ROWS;
     const bool db16 = d->k > 8 && lds_db <= kLdsPerCu;   /* 16+4 heal / row-masked encode */
+    /* the 16-row decode of a 16+4 volume: 4-stripe tiles (half the LDS).
+     * Pinned 16+4 decodes (profiles/r04/r04s_zcheal.log, one tile per block
+     * -> this): 16 MiB 570-576 -> 525 us, 64 MiB 1793-1797 -> 1639; at 4 MiB
+     * 172 -> 177, so calls below 2048 stripes (16 MiB) keep ec_combine_zc */
+    const size_t lds_db4 = (size_t)(2 * d->k + d->rows) * 4 * ECD_CHUNK + 8 * ECD_MAX_ROWS;
+    const bool db16t4 = d->k > 8 && !db16 && a.nstripes >= 2048 &&
+                        lds_db4 <= (128u << 10) + 8 * ECD_MAX_ROWS;
+    if (zc_double_buffered() && db16t4) {
+        const uint64_t g4 = (a.nstripes + 3) / 4;
+        const uint64_t tpb = zc_fixed_tpb();
+        const uint64_t want = tpb ? g4 / tpb
+                                  : std::min<uint64_t>(g4 / 2, zc_inflight_bytes() /
+                                                                   ((uint64_t)d->k * 4 * ECD_CHUNK));
+        const uint64_t gdb = std::min<uint64_t>(std::max<uint64_t>(want, 1), (uint64_t)cu_count());
+        const void *kern = a.group_pattern ? (const void *)ec_combine_zc_db<16, NW, true, 4>
+                                           : (const void *)ec_combine_zc_db<16, NW, false, 4>;
+        if (lds_db4 > (64u << 10) &&
+            ensure_lds_limit(kern, (int)((128u << 10) + 8 * ECD_MAX_ROWS)) != 0)
+            return -EIO;
+        void *args[] = {&a};
+        if (hipLaunchKernel(kern, dim3((u32)gdb), dim3(NW * 64), args, lds_db4, s) != hipSuccess)
+            return -EIO;
+        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    }
     if (zc_double_buffered() &&
         ((d->k <= 8 && lds_db <= (128u << 10) + 8 * ECD_MAX_ROWS) || db16)) {
         /* persistent, at most one block per CU, >= 2 tiles per block so its

@@ -1435,10 +1435,14 @@ __device__ __forceinline__ v4u lds_read_b128(const uint8_t *p)
     return v;
 }
 
-template <int K, int NW, bool MIXED>
+template <int K, int NW, bool MIXED, int TT = 8>
 __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
 {
-    constexpr u32 T = 8;
+    /* TT stripes per tile: 8 (lanes hold 2 dwords of a plane), or 4 for the
+     * 16-row decode of a 16+4 volume, whose two 8-stripe input tiles and
+     * output tile would not fit the CU's LDS (lanes hold 1 dword) */
+    constexpr u32 T = TT, CW = TT / 4, LPS = 64 / TT;   /* lanes per stripe */
+    static_assert(TT == 4 || TT == 8, "4- or 8-stripe tiles");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
     const u32 k = a.k, rows = a.rows;
@@ -1483,23 +1487,25 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
     __builtin_amdgcn_s_waitcnt(0x0070);        /* vmcnt(0) lgkmcnt(0) */
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const u32 cs = lane >> 3, cc = lane & 7u;
+    const u32 cs = lane / LPS, cc = lane % LPS;
     for (u32 i = 0;; ++i) {
         const uint64_t t0 = t * T;
         const uint8_t *buf = lds + (i & 1u) * tb;
         {
             const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
             for (u32 r = wave; r < rows; r += NW) {
-                const uint8_t *col = buf + cs * ECD_CHUNK + cc * 8u;
+                const uint8_t *col = buf + cs * ECD_CHUNK + cc * (4u * CW);
                 const u32 rw = a.kw * (1 + r);
                 const u32 w0 = pw.word(a, rw);
                 const u32 w1 = K > 4 ? pw.word(a, rw + 1) : 0u;
                 const u32 w2 = K > 8 ? pw.word(a, rw + 2) : 0u;
                 const u32 w3 = K > 12 ? pw.word(a, rw + 3) : 0u;
-                u32 acc[8][2], y[8][2];
+                u32 acc[8][CW], y[8][CW];
 #pragma unroll
                 for (int b = 0; b < 8; ++b)
-                    acc[b][0] = acc[b][1] = 0;
+#pragma unroll
+                    for (u32 w = 0; w < CW; ++w)
+                        acc[b][w] = 0;
                 /* one coefficient byte per input, shifted out of a 64-bit
                  * (K <= 8) or 128-bit (K = 16) scalar register pair */
                 uint64_t cl = (uint64_t)w0 | ((uint64_t)w1 << 32);
@@ -1514,13 +1520,17 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
                     const uint8_t *src = col + p * (T * ECD_CHUNK);
 #pragma unroll
                     for (int b = 0; b < 8; ++b)
-                        load_plane<2>(src + (u32)b * 64u, y[b]);
-                    ecgf::mul_xor_rt<2>(c, acc, y);
+                        load_plane<CW>(src + (u32)b * 64u, y[b]);
+                    ecgf::mul_xor_rt<CW>(c, acc, y);
                 }
-                uint8_t *o = otile + (r * T + cs) * ECD_CHUNK + cc * 8u;
+                uint8_t *o = otile + (r * T + cs) * ECD_CHUNK + cc * (4u * CW);
 #pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+                for (int b = 0; b < 8; ++b) {
+                    if constexpr (CW == 2)
+                        *reinterpret_cast<uint2 *>(o + b * 64) = make_uint2(acc[b][0], acc[b][1]);
+                    else
+                        *reinterpret_cast<u32 *>(o + b * 64) = acc[b][0];
+                }
             }
         }
         asm volatile("" ::: "memory");

@@ -167,6 +167,40 @@ def test_decode_mixed_small_groups_host_kinds(ec, oracle, kind):
         p.close()
 
 
+@pytest.mark.parametrize("kind", ["pinned", "pageable"])
+@pytest.mark.parametrize("group", [8, 16])
+def test_decode_16p4_host_kinds(ec, oracle, kind, group):
+    """16+4 decodes of host buffers: the 16-row combine runs the persistent
+    zero-copy kernel on 4-stripe tiles (two 8-stripe input tiles and the
+    output tile would not fit the CU's LDS), single-pattern and mixed with
+    8- and 16-stripe pattern groups, ragged ends."""
+    k, n = 16, 20
+    nst = 3 * 1024 + 13           # >= 2048 stripes: the 4-stripe persistent kernel
+    data = rand_bytes(CHUNK * k * nst, seed=group + 31)
+    enc = oracle.encode(k, n, data, nthreads=8)
+    p = Bufs(ec, kind)
+    try:
+        frags = [p.new(CHUNK * nst, enc[i]) for i in range(n)]
+        out = p.new(data.size, 0)
+        rng = np.random.default_rng(group)
+        pool_masks = [0xFFFF0, 0x0FFFF, 0xF0FFF, 0xFF0FF, 0x7FFF8]
+        ngroups = (nst + group - 1) // group
+        masks = [pool_masks[i] for i in rng.integers(0, len(pool_masks), ngroups)]
+        s0 = ec.ec_method.stats()
+        with ec.ECMatrixList(k, n) as L:
+            for m in pool_masks[:2]:
+                rows = [b + 1 for b in range(n) if (m >> b) & 1]
+                out[:] = 0
+                L.decode_batch(nst, m, rows, [frags[r - 1] for r in rows], out)
+                assert np.array_equal(out, data), hex(m)
+            out[:] = 0
+            L.decode_mixed(nst, group, masks, frags, out)
+            assert np.array_equal(out, data)
+        assert ec.ec_method.stats()["cpu_fallbacks"] == s0["cpu_fallbacks"]
+    finally:
+        p.close()
+
+
 def test_register_errors(ec):
     import ctypes
     lib = ec.ec_method.lib
