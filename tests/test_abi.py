@@ -123,6 +123,29 @@ def test_pool_and_deferred_registration_without_gpu():
     assert not b.pooled and b.array.nbytes == 8192
 
 
+def test_encode_rows_device_argument_errors_without_gpu():
+    """ec_method_encode_rows_device: bits beyond the volume's bricks and NULL
+    output slots of selected bricks are -EINVAL before any device work; an
+    empty mask or zero stripes are no-ops; a real request without a device is
+    -ENODEV (device-resident entry points have no CPU path to fall back to)."""
+    import errno
+    import glusterfs_amd as g
+    if g.device_count() > 0:
+        pytest.skip("GPU visible")
+    with g.ECMatrixList(4, 6) as L:
+        lib = g.ec_method.lib
+        src = (ctypes.c_uint8 * (512 * 4))()
+        dst = [(ctypes.c_uint8 * 512)() for _ in range(6)]
+        outs = (ctypes.c_void_p * 6)(*[ctypes.addressof(d) for d in dst])
+        call = lambda nst, m, o: lib.ec_method_encode_rows_device(  # noqa: E731
+            ctypes.byref(L._list), 0, None, nst, ctypes.addressof(src), m, o)
+        assert call(1, 1 << 6, outs) == -errno.EINVAL
+        holes = (ctypes.c_void_p * 6)(None, *[ctypes.addressof(d) for d in dst[1:]])
+        assert call(1, 0x1, holes) == -errno.EINVAL
+        assert call(1, 0, outs) == 0 and call(0, 0x3, outs) == 0
+        assert call(1, 0x3, outs) == -errno.ENODEV
+
+
 def test_host_matrices_match_oracle(oracle):
     import glusterfs_amd as g
     for k, n in ((2, 3), (4, 6), (8, 12), (16, 20), (16, 31), (5, 7)):
