@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Differential fuzzer of the drop-in API against the oracle (development
+tool, GPU box; runs on the CPU engine too).
+
+For FUZZ_SECS seconds (default 120), FUZZ_THREADS threads (default 8) draw
+random calls -- geometry k+r (k 2..16), size (1 stripe .. ~4 MiB), buffer
+kind (device tensor, pinned, pool, pageable, misaligned pinned) and entry
+point (encode, encode_rows, decode, decode_mixed, heal, writev_encode) -- run
+them through glusterfs_amd (ctypes over libec_mi355x.so) and compare every
+output byte with the oracle's (oracle/, the test checker).  Buffers of a call
+share one kind (mixing host and device is -EINVAL by contract; mixing host
+kinds is what the pool / pinned / pageable draws across calls exercise).
+Prints a progress line every ~10 s and one JSON summary; exit status 1 on
+the first mismatch (its parameters are printed, and FUZZ_SEED replays it).
+EC_GPU_ALWAYS=1 keeps host calls on the GPU.  Usage: python tools/fuzz_api.py"""
+import json
+import os
+import random
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401  (torch first: one HIP runtime)
+import glusterfs_amd as g  # noqa: E402
+import oracle as O  # noqa: E402  (the checker)
+
+CHUNK = 512
+GEOS = [(2, 1), (3, 2), (4, 2), (5, 2), (6, 3), (8, 4), (8, 3), (10, 4), (12, 4), (16, 4), (16, 8)]
+OPS = ["encode", "encode_rows", "decode", "decode_mixed", "heal", "writev"]
+
+
+class Arena:
+    """Buffers of one kind for one call; freed together."""
+
+    def __init__(self, kind, dev):
+        self.kind, self.dev, self.keep = kind, dev, []
+
+    def buf(self, data=None, nbytes=None):
+        n = data.size if data is not None else nbytes
+        if self.kind == "device":
+            t = torch.empty(n, dtype=torch.uint8, device=self.dev)
+            if data is not None:
+                t.copy_(torch.from_numpy(data))
+            return t
+        if self.kind in ("pinned", "misaligned"):
+            extra = 8 if self.kind == "misaligned" else 0
+            p = g.PinnedArray(n + extra)
+            self.keep.append(p)
+            a = p.array[extra:extra + n]
+        elif self.kind == "pool":
+            p = g.PoolBuffer(n)
+            self.keep.append(p)
+            a = p.array[:n]
+        else:
+            a = np.empty(n, np.uint8)
+        if data is not None:
+            a[:] = data
+        return a
+
+    def free(self):
+        for p in self.keep:
+            p.free()
+
+
+def host(x):
+    return x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
+
+
+def one_call(rng, lists, dev):
+    k, r = rng.choice(GEOS)
+    n = k + r
+    L = lists[(k, r)]
+    op = rng.choice(OPS)
+    kinds = ["device", "pinned", "pool", "pageable", "misaligned"] if dev is not None else \
+        ["pool", "pageable"]
+    kind = rng.choice(kinds)
+    if op in ("writev", "decode_mixed") and kind == "device":
+        kind = "pinned"          # host entry points (their _device forms take other args)
+    nst = rng.choice([1, 2, 7, 8, 9, 31, 64, 100, 257, 1000, 1031,
+                      max(1, (4 << 20) // (CHUNK * k))])
+    seed = rng.randrange(1 << 30)
+    drng = np.random.default_rng(seed)
+    data = drng.integers(0, 256, CHUNK * k * nst, dtype=np.uint8)
+    desc = dict(op=op, k=k, n=n, kind=kind, nst=nst, seed=seed)
+    A = Arena(kind, dev)
+    try:
+        if op == "encode":
+            src = A.buf(data)
+            outs = [A.buf(nbytes=CHUNK * nst) for _ in range(n)]
+            L.encode_batch(nst, src, outs)
+            want = O.encode(k, n, data)
+            return desc, all(np.array_equal(host(o), w) for o, w in zip(outs, want))
+        if op == "encode_rows":
+            m = rng.randrange(1, 1 << n)
+            desc["mask"] = m
+            src = A.buf(data)
+            outs = [A.buf(nbytes=CHUNK * nst) if (m >> i) & 1 else None for i in range(n)]
+            if kind == "device":
+                L.encode_rows_device(dev.index, None, nst, src, m, outs)
+                g.sync_device(dev.index)
+            else:
+                L.encode_rows(data.size, src, m, outs)
+            want = O.encode(k, n, data)
+            return desc, all(np.array_equal(host(o), want[i]) for i, o in enumerate(outs)
+                             if o is not None)
+        frags_np = [drng.integers(0, 256, CHUNK * nst, dtype=np.uint8) for _ in range(n)]
+        rows = sorted(rng.sample(range(1, n + 1), k))
+        mask = sum(1 << (x - 1) for x in rows)
+        desc["mask"] = mask
+        if op == "decode":
+            fr = [A.buf(frags_np[x - 1]) for x in rows]
+            out = A.buf(nbytes=CHUNK * k * nst)
+            L.decode_batch(nst, mask, rows, fr, out)
+            return desc, np.array_equal(host(out), O.decode(k, rows, [frags_np[x - 1]
+                                                                      for x in rows]))
+        if op == "heal":
+            fr = [A.buf(frags_np[x - 1]) for x in rows]
+            lost = [b for b in range(n) if not (mask >> b) & 1]
+            tgt = rng.sample(lost, rng.randint(1, len(lost)))
+            tmask = sum(1 << b for b in tgt)
+            outs = [A.buf(nbytes=CHUNK * nst) for _ in tgt]
+            L.heal(nst, mask, fr, tmask, outs)
+            full = O.encode(k, n, O.decode(k, rows, [frags_np[x - 1] for x in rows]))
+            return desc, all(np.array_equal(host(o), full[b])
+                             for o, b in zip(outs, sorted(tgt)))
+        if op == "decode_mixed":
+            grp = rng.choice([1, 2, 4, 8, 16, 64])
+            ng = (nst + grp - 1) // grp
+            pool_masks = [mask] + [sum(1 << (x - 1) for x in sorted(rng.sample(range(1, n + 1), k)))
+                                   for _ in range(rng.randint(0, 5))]
+            gm = [rng.choice(pool_masks) for _ in range(ng)]
+            fr = [A.buf(f) for f in frags_np]
+            out = A.buf(nbytes=CHUNK * k * nst)
+            L.decode_mixed(nst, grp, gm, fr, out)
+            got = host(out)
+            for gi, m in enumerate(gm):
+                a0, a1 = gi * grp * CHUNK, min(nst, (gi + 1) * grp) * CHUNK
+                rw = O.mask_rows(m)
+                exp = O.decode(k, rw, [frags_np[x - 1][a0:a1] for x in rw])
+                if not np.array_equal(got[a0 * k:a1 * k], exp):
+                    return desc, False
+            return desc, True
+        # writev: a partial-stripe write at a random head with old stripes
+        S = CHUNK * k
+        head = rng.randrange(S)
+        us = rng.randrange(1, max(2, CHUNK * k * nst - head))
+        user = data[:us]
+        oh = drng.integers(0, 256, S, dtype=np.uint8) if rng.random() < 0.7 else None
+        ot = drng.integers(0, 256, S, dtype=np.uint8) if rng.random() < 0.7 else None
+        desc.update(head=head, user=us)
+        size = (head + us + S - 1) // S * S
+        outs = [A.buf(nbytes=size // k) for _ in range(n)]
+        L.writev_encode(head, A.buf(user), None if oh is None else A.buf(oh),
+                        None if ot is None else A.buf(ot), outs)
+        want = O.encode(k, n, O.writev_merge(k, head, user, oh, ot))
+        return desc, all(np.array_equal(host(o), w) for o, w in zip(outs, want))
+    finally:
+        A.free()
+
+
+def main():
+    secs = float(os.environ.get("FUZZ_SECS", "120"))
+    nth = int(os.environ.get("FUZZ_THREADS", "8"))
+    seed0 = int(os.environ.get("FUZZ_SEED", str(int(time.time()))))
+    dev = torch.device("cuda:0") if g.device_count() > 0 else None
+    lists = {gk: g.ECMatrixList(gk[0], gk[0] + gk[1]) for gk in GEOS}
+    counts = {op: 0 for op in OPS}
+    bad = []
+    lock = threading.Lock()
+    t_end = time.time() + secs
+
+    def worker(t):
+        rng = random.Random(seed0 * 1000 + t)
+        while time.time() < t_end and not bad:
+            try:
+                desc, ok = one_call(rng, lists, dev)
+            except Exception as e:  # noqa: BLE001 -- any error is a finding
+                desc, ok = dict(error=repr(e)[:300]), False
+            with lock:
+                if ok:
+                    counts[desc["op"]] += 1
+                else:
+                    bad.append(desc)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(nth)]
+    for t in th:
+        t.start()
+    last = time.time()
+    while any(t.is_alive() for t in th):
+        time.sleep(0.5)
+        if time.time() - last >= 10:
+            last = time.time()
+            print("fuzz: %d calls, %d bad" % (sum(counts.values()), len(bad)), flush=True)
+    for t in th:
+        t.join()
+    st = g.ec_method.stats()
+    for L in lists.values():
+        L.fini()
+    print(json.dumps(dict(seed=seed0, threads=nth, secs=secs, calls=counts,
+                          gpu_calls=st["gpu_calls"], cpu_calls=st["cpu_calls"],
+                          cpu_fallbacks=st["cpu_fallbacks"], mismatches=bad[:5])), flush=True)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -5,7 +5,7 @@
 # Steps: smoke | pytest | pytest_new (the files in $TESTS) | bench | bench_rocprof
 #        | rehearsal (2 gloo ranks on GPU 0) | profile (per-config rocprof + PMC)
 #        | kbench (tools/kbench/kbench $KBENCH_ARGS) | kb3 (tools/kbench/kb3 $KB3_ARGS)
-#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | zcheal (pinned 16+4 / 8+4 decode, encode, heal, row-masked encode, ZCDB A/B) | pcie (DMA copy ceiling of the link, each way and duplex) | zctpb (pinned decodes + encodes 1-256 MiB by EC_ZC_TPB / EC_ZC_INFLIGHT_KB) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | ablib (tools/ab_lib.sh: two library builds alternating through bench.py --only) | concur (tools/kbench/concur: concurrent vs coalesced-ceiling calls, auto / gpu / cpu) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
+#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | zcheal (pinned 16+4 / 8+4 decode, encode, heal, row-masked encode, ZCDB A/B) | fuzz (tools/fuzz_api.py: random calls of every entry point and buffer kind against the oracle, GPU-always then auto) | pcie (DMA copy ceiling of the link, each way and duplex) | zctpb (pinned decodes + encodes 1-256 MiB by EC_ZC_TPB / EC_ZC_INFLIGHT_KB) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | ablib (tools/ab_lib.sh: two library builds alternating through bench.py --only) | concur (tools/kbench/concur: concurrent vs coalesced-ceiling calls, auto / gpu / cpu) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
 # Logs go to gpurun_out/${TAG}_<step>.log.
 set -u
 mkdir -p gpurun_out
@@ -34,6 +34,7 @@ for step in "$@"; do
     zcsizes) run zcsizes 600 bash -c 'for r in 1 2; do for v in 0 1; do EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v python3 tools/zc_sizes.py || exit 1; done; done' ;;
     zctpb) run zctpb 900 bash -c 'for r in 1 2; do for c in "0 2048" "4 2048" "0 1024" "0 4096"; do set -- $c; EC_GPU_ALWAYS=1 EC_ZC_TPB=$1 EC_ZC_INFLIGHT_KB=$2 ZC_SIZES="${ZC_SIZES:-1 2 4 8 16 64 256}" python3 tools/zc_sizes.py || exit 1; done; done' ;;
     zcheal) run zcheal 600 bash -c 'for r in 1 2; do for v in 0 1; do EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v ZC_GEOS="16+4 8+4" ZC_SIZES="4 16 64" python3 tools/zc_sizes.py || exit 1; done; done' ;;
+    fuzz) run fuzz 420 bash -c 'EC_GPU_ALWAYS=1 FUZZ_SECS=${FUZZ_SECS:-150} python3 -u tools/fuzz_api.py && EC_GPU_ALWAYS=0 FUZZ_SECS=60 python3 -u tools/fuzz_api.py' ;;
     pcie) run pcie 200 bash -c 'for m in 4 16 256; do python3 tools/pcie_probe.py $m || exit 1; done' ;;
     hsweep) run hsweep 300 bash -c "cd /tmp && export TMPDIR=/tmp && EC_GPU_ALWAYS=1 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_hsweep_$TAG -o run --output-format csv -- python3 $R/bench.py --heal-sweep gpu --steps 64 && python3 $R/tools/prof_filter.py $R/gpurun_out/prof_hsweep_$TAG ec_ && python3 $R/tools/trace_seq.py $R/gpurun_out/prof_hsweep_$TAG" ;;
     hostlat) run hostlat 180 python -u tools/host_latency.py ;;
