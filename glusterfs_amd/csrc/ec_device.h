@@ -72,6 +72,12 @@ int ecd_sync(int device, void *stream);
  * exists for k+n. */
 int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes,
                     const void *in, void *const *out, const uint8_t *enc_pat);
+/* The same for `rows` arbitrary encode-matrix rows (ec_method_encode_rows):
+ * always the generic combination with `pat` (k + rows*k bytes), never the
+ * specialised encoders -- rows == 20 of a 16+8 volume are not the 16+4
+ * Vandermonde rows. */
+int ecd_encode_host_rows(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes,
+                         const void *in, void *const *out, const uint8_t *pat);
 
 /* Encode of a virtual input: the concatenation of nsegs segments
  * (seg_ptr[i] == NULL: seg_len[i] zero bytes), nstripes*k*512 bytes in

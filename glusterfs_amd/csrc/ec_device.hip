@@ -1020,12 +1020,13 @@ struct EncodeJob {
     uint8_t *const *out;    /* n whole fragment buffers                   */
     const uint8_t *enc_pat; /* generic coefficients (k + n*k bytes)       */
     uint64_t s0, s1;        /* stripe range of this device                */
+    bool generic;           /* rows of enc_pat, not the k+n Vandermonde   */
 };
 
 int launch_encode(hipStream_t st, const EncodeJob &j, const uint8_t *din, uint8_t *const *outs,
                   uint64_t cnt)
 {
-    if (ecdk_has_vander(j.k, j.n)) /* host buffers: the zero-copy kernel */
+    if (!j.generic && ecdk_has_vander(j.k, j.n)) /* host buffers: the zero-copy kernel */
         return ecdk_encode_vander(st, j.k, j.n, cnt, din, (void *const *)outs, true);
     ecd_combine_desc_t d;
     memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
@@ -1362,11 +1363,13 @@ int ecd_sync(int device, void *stream)
 }
 
 static int encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const void *in,
-                       const std::vector<Seg> *gather, void *const *out, const uint8_t *enc_pat)
+                       const std::vector<Seg> *gather, void *const *out, const uint8_t *enc_pat,
+                       bool generic = false)
 {
     if (ecd_device_count() == 0)
         return -ENODEV;
     EncodeJob base;
+    base.generic = generic;
     base.k = k;
     base.n = n;
     base.in = static_cast<const uint8_t *>(in);
@@ -1386,6 +1389,14 @@ int ecd_encode_host(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, const v
                     void *const *out, const uint8_t *enc_pat)
 {
     return encode_host(ndev, k, n, nstripes, in, nullptr, out, enc_pat);
+}
+
+int ecd_encode_host_rows(int ndev, uint32_t k, uint32_t rows, uint64_t nstripes, const void *in,
+                         void *const *out, const uint8_t *pat)
+{
+    if (!pat || rows == 0 || rows > ECD_MAX_ROWS || k == 0 || k > ECD_MAX_K)
+        return -EINVAL;
+    return encode_host(ndev, k, rows, nstripes, in, nullptr, out, pat, true);
 }
 
 int ecd_encode_host_gather(int ndev, uint32_t k, uint32_t n, uint64_t nstripes, uint32_t nsegs,

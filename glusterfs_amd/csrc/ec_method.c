@@ -1348,7 +1348,7 @@ host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
 
     if (!route_cpu(ctx, user, bytes, ECM_DECODE, 0) &&
         !route_cpu(ctx, user, bytes, ECM_DECODE, enc_staged(&eb))) {
-        rc = ecd_encode_host(0, ctx->k, m, nstripes, in, outs, pat);
+        rc = ecd_encode_host_rows(0, ctx->k, m, nstripes, in, outs, pat);
         if (!gpu_failed(rc)) {
             if (rc == 0)
                 stat_add(ECM_STAT_GPU);

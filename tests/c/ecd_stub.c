@@ -18,6 +18,9 @@ int ecd_sync(int d, void *s) { (void)d; (void)s; return -ENODEV; }
 int ecd_encode_host(int nd, uint32_t k, uint32_t n, uint64_t ns, const void *in, void *const *out,
                     const uint8_t *p)
 { (void)nd; (void)k; (void)n; (void)ns; (void)in; (void)out; (void)p; return -ENODEV; }
+int ecd_encode_host_rows(int nd, uint32_t k, uint32_t r, uint64_t ns, const void *in,
+                         void *const *out, const uint8_t *p)
+{ (void)nd; (void)k; (void)r; (void)ns; (void)in; (void)out; (void)p; return -ENODEV; }
 int ecd_encode_host_gather(int nd, uint32_t k, uint32_t n, uint64_t ns, uint32_t sg,
                            const void *const *sp, const uint64_t *sl, void *const *out,
                            const uint8_t *p)

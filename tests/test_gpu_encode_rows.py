@@ -138,3 +138,43 @@ def test_encode_rows_device_async(oracle, k, n):
                 assert (got == 0x5A).all()
         with pytest.raises(OSError):
             L.encode_rows_device(0, st.cuda_stream, nst, din, 1 << n, outs)
+
+
+@pytest.mark.parametrize("k,r,rows", [(16, 8, 20), (4, 3, 6), (8, 5, 12), (2, 2, 3)])
+@pytest.mark.parametrize("kind", ["pinned", "pageable"])
+def test_encode_rows_count_of_a_specialised_geometry(oracle, k, r, rows, kind):
+    """Regression (tools/fuzz_api.py, r04u): a row-masked encode whose row
+    count equals the n of a geometry with a specialised encoder (20 rows of
+    a 16+8 volume, 6 of a 4+3, ...) took that encoder, i.e. the first n
+    Vandermonde rows instead of the selected ones.  The host path now always
+    runs the generic combination with the selected rows."""
+    import glusterfs_amd as g
+    n = k + r
+    nst = 1031
+    data = rnd(CHUNK * k * nst, k * 13 + r)
+    want = oracle.encode(k, n, data)
+    rng = np.random.default_rng(rows)
+    keep = []
+    try:
+        def buf(nb):
+            if kind == "pinned":
+                p = g.PinnedArray(nb)
+                keep.append(p)
+                return p.array
+            return np.empty(nb, np.uint8)
+        src = buf(data.size)
+        src[:] = data
+        with g.ECMatrixList(k, n) as L:
+            for _ in range(3):
+                pick = sorted(rng.choice(n, rows, replace=False))
+                if list(pick) == list(range(rows)):
+                    pick = list(range(n - rows, n))
+                m = sum(1 << int(b) for b in pick)
+                outs = [buf(CHUNK * nst) if (m >> i) & 1 else None for i in range(n)]
+                L.encode_rows(data.size, src, m, outs)
+                for i, o in enumerate(outs):
+                    if o is not None:
+                        assert np.array_equal(o, want[i]), (k, n, hex(m), i)
+    finally:
+        for p in keep:
+            p.free()
