@@ -5,7 +5,9 @@ tool, GPU box; runs on the CPU engine too).
 For FUZZ_SECS seconds (default 120), FUZZ_THREADS threads (default 8) draw
 random calls -- geometry k+r (k 2..16), size (1 stripe .. ~4 MiB), buffer
 kind (device tensor, pinned, pool, pageable, misaligned pinned) and entry
-point (encode, encode_rows, decode, decode_mixed, heal, writev_encode) -- run
+point (encode, encode_rows, decode, decode_mixed, heal, writev_encode, and
+the reference's own size-based encode + decode pair; device buffers go
+through the _device forms where they differ) -- run
 them through glusterfs_amd (ctypes over libec_mi355x.so) and compare every
 output byte with the oracle's (oracle/, the test checker).  Buffers of a call
 share one kind (mixing host and device is -EINVAL by contract; mixing host
@@ -31,7 +33,7 @@ import oracle as O  # noqa: E402  (the checker)
 
 CHUNK = 512
 GEOS = [(2, 1), (3, 2), (4, 2), (5, 2), (6, 3), (8, 4), (8, 3), (10, 4), (12, 4), (16, 4), (16, 8)]
-OPS = ["encode", "encode_rows", "decode", "decode_mixed", "heal", "writev"]
+OPS = ["encode", "encode_rows", "decode", "decode_mixed", "heal", "writev", "dropin"]
 
 
 class Arena:
@@ -79,8 +81,7 @@ def one_call(rng, lists, dev):
     kinds = ["device", "pinned", "pool", "pageable", "misaligned"] if dev is not None else \
         ["pool", "pageable"]
     kind = rng.choice(kinds)
-    if op in ("writev", "decode_mixed") and kind == "device":
-        kind = "pinned"          # host entry points (their _device forms take other args)
+
     nst = rng.choice([1, 2, 7, 8, 9, 31, 64, 100, 257, 1000, 1031,
                       max(1, (4 << 20) // (CHUNK * k))])
     seed = rng.randrange(1 << 30)
@@ -95,6 +96,20 @@ def one_call(rng, lists, dev):
             L.encode_batch(nst, src, outs)
             want = O.encode(k, n, data)
             return desc, all(np.array_equal(host(o), w) for o, w in zip(outs, want))
+        if op == "dropin":
+            # the reference's own two calls (ec-method.h:31-46): encode by
+            # size, then decode by fragment size from a random brick set
+            src = A.buf(data)
+            outs = [A.buf(nbytes=CHUNK * nst) for _ in range(n)]
+            L.encode(data.size, src, outs)
+            rows = sorted(rng.sample(range(1, n + 1), k))
+            m = sum(1 << (x - 1) for x in rows)
+            desc["mask"] = m
+            out = A.buf(nbytes=data.size)
+            L.decode(CHUNK * nst, m, rows, [outs[x - 1] for x in rows], out)
+            want = O.encode(k, n, data)
+            return desc, np.array_equal(host(out), data) and all(
+                np.array_equal(host(o), w) for o, w in zip(outs, want))
         if op == "encode_rows":
             m = rng.randrange(1, 1 << n)
             desc["mask"] = m
@@ -136,7 +151,13 @@ def one_call(rng, lists, dev):
             gm = [rng.choice(pool_masks) for _ in range(ng)]
             fr = [A.buf(f) for f in frags_np]
             out = A.buf(nbytes=CHUNK * k * nst)
-            L.decode_mixed(nst, grp, gm, fr, out)
+            if kind == "device":
+                uniq = sorted(set(gm))
+                ids = torch.tensor([uniq.index(x) for x in gm], dtype=torch.uint8, device=dev)
+                L.decode_mixed_device(dev.index, None, nst, grp, ids, uniq, fr, out)
+                g.sync_device(dev.index)
+            else:
+                L.decode_mixed(nst, grp, gm, fr, out)
             got = host(out)
             for gi, m in enumerate(gm):
                 a0, a1 = gi * grp * CHUNK, min(nst, (gi + 1) * grp) * CHUNK
@@ -155,8 +176,14 @@ def one_call(rng, lists, dev):
         desc.update(head=head, user=us)
         size = (head + us + S - 1) // S * S
         outs = [A.buf(nbytes=size // k) for _ in range(n)]
-        L.writev_encode(head, A.buf(user), None if oh is None else A.buf(oh),
-                        None if ot is None else A.buf(ot), outs)
+        if kind == "device":
+            L.writev_encode_device(dev.index, None, head, us, A.buf(user),
+                                   None if oh is None else A.buf(oh),
+                                   None if ot is None else A.buf(ot), outs)
+            g.sync_device(dev.index)
+        else:
+            L.writev_encode(head, A.buf(user), None if oh is None else A.buf(oh),
+                            None if ot is None else A.buf(ot), outs)
         want = O.encode(k, n, O.writev_merge(k, head, user, oh, ot))
         return desc, all(np.array_equal(host(o), w) for o, w in zip(outs, want))
     finally:
