@@ -4,7 +4,8 @@ tool, GPU box; runs on the CPU engine too).
 
 For FUZZ_SECS seconds (default 120), FUZZ_THREADS threads (default 8) draw
 random calls -- geometry k+r (k 2..16), size (1 stripe .. ~4 MiB), buffer
-kind (device tensor, pinned, pool, pageable, misaligned pinned) and entry
+kind (device tensor, device tensor at an odd byte offset, pinned, registered
+range, pool, pageable, misaligned pinned) and entry
 point (encode, encode_rows, decode, decode_mixed, heal, writev_encode, and
 the reference's own size-based encode + decode pair; device buffers go
 through the _device forms where they differ) -- run
@@ -40,16 +41,28 @@ class Arena:
     """Buffers of one kind for one call; freed together."""
 
     def __init__(self, kind, dev):
-        self.kind, self.dev, self.keep = kind, dev, []
+        self.kind, self.dev, self.keep, self.regs, self.keep_raw = kind, dev, [], [], []
 
     def buf(self, data=None, nbytes=None):
         n = data.size if data is not None else nbytes
-        if self.kind == "device":
-            t = torch.empty(n, dtype=torch.uint8, device=self.dev)
+        if self.kind in ("device", "device_offset"):
+            off = 3 if self.kind == "device_offset" else 0   # a tensor slice at an odd byte
+            t = torch.empty(n + off, dtype=torch.uint8, device=self.dev)[off:]
             if data is not None:
                 t.copy_(torch.from_numpy(data))
             return t
-        if self.kind in ("pinned", "misaligned"):
+        if self.kind == "registered":     # an existing range registered (an iobuf arena)
+            raw = np.empty(n + 8192, np.uint8)
+            a = raw[(-raw.ctypes.data) % 4096:][:n + 4096]
+            rc = g.ec_method.lib.ec_method_host_register(a.ctypes.data, a.nbytes)
+            if rc == 0:
+                self.regs.append(a.ctypes.data)
+            self.keep_raw.append(raw)
+            a = a[:n]
+            if data is not None:
+                a[:] = data
+            return a
+        if self.kind in ("pinned", "misaligned"):  # noqa: SIM114
             extra = 8 if self.kind == "misaligned" else 0
             p = g.PinnedArray(n + extra)
             self.keep.append(p)
@@ -67,6 +80,8 @@ class Arena:
     def free(self):
         for p in self.keep:
             p.free()
+        for p in self.regs:
+            g.ec_method.lib.ec_method_host_unregister(p)
 
 
 def host(x):
@@ -78,8 +93,8 @@ def one_call(rng, lists, dev):
     n = k + r
     L = lists[(k, r)]
     op = rng.choice(OPS)
-    kinds = ["device", "pinned", "pool", "pageable", "misaligned"] if dev is not None else \
-        ["pool", "pageable"]
+    kinds = ["device", "device_offset", "pinned", "registered", "pool", "pageable",
+             "misaligned"] if dev is not None else ["pool", "pageable"]
     kind = rng.choice(kinds)
 
     nst = rng.choice([1, 2, 7, 8, 9, 31, 64, 100, 257, 1000, 1031,
@@ -115,7 +130,7 @@ def one_call(rng, lists, dev):
             desc["mask"] = m
             src = A.buf(data)
             outs = [A.buf(nbytes=CHUNK * nst) if (m >> i) & 1 else None for i in range(n)]
-            if kind == "device":
+            if kind.startswith("device"):
                 L.encode_rows_device(dev.index, None, nst, src, m, outs)
                 g.sync_device(dev.index)
             else:
@@ -151,7 +166,7 @@ def one_call(rng, lists, dev):
             gm = [rng.choice(pool_masks) for _ in range(ng)]
             fr = [A.buf(f) for f in frags_np]
             out = A.buf(nbytes=CHUNK * k * nst)
-            if kind == "device":
+            if kind.startswith("device"):
                 uniq = sorted(set(gm))
                 ids = torch.tensor([uniq.index(x) for x in gm], dtype=torch.uint8, device=dev)
                 L.decode_mixed_device(dev.index, None, nst, grp, ids, uniq, fr, out)
@@ -176,7 +191,7 @@ def one_call(rng, lists, dev):
         desc.update(head=head, user=us)
         size = (head + us + S - 1) // S * S
         outs = [A.buf(nbytes=size // k) for _ in range(n)]
-        if kind == "device":
+        if kind.startswith("device"):
             L.writev_encode_device(dev.index, None, head, us, A.buf(user),
                                    None if oh is None else A.buf(oh),
                                    None if ot is None else A.buf(ot), outs)
