@@ -88,6 +88,18 @@ def host(x):
     return x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
 
 
+def same(desc, name, got, want):
+    """Byte equality; on a difference, note where in desc (first offset,
+    count, and whether the buffer holds the oracle's bytes elsewhere)."""
+    got = host(got)
+    if np.array_equal(got, want):
+        return True
+    d = np.nonzero(got != want)[0]
+    desc.setdefault("diff", []).append(dict(buf=name, first=int(d[0]), count=int(d.size),
+                                            size=int(want.size), zeros=bool((got == 0).all())))
+    return False
+
+
 def one_call(rng, lists, dev):
     k, r = rng.choice(GEOS)
     n = k + r
@@ -110,7 +122,7 @@ def one_call(rng, lists, dev):
             outs = [A.buf(nbytes=CHUNK * nst) for _ in range(n)]
             L.encode_batch(nst, src, outs)
             want = O.encode(k, n, data)
-            return desc, all(np.array_equal(host(o), w) for o, w in zip(outs, want))
+            return desc, all([same(desc, "frag%d" % i, o, w) for i, (o, w) in enumerate(zip(outs, want))])
         if op == "dropin":
             # the reference's own two calls (ec-method.h:31-46): encode by
             # size, then decode by fragment size from a random brick set
@@ -121,10 +133,10 @@ def one_call(rng, lists, dev):
             m = sum(1 << (x - 1) for x in rows)
             desc["mask"] = m
             out = A.buf(nbytes=data.size)
-            L.decode(CHUNK * nst, m, rows, [outs[x - 1] for x in rows], out)
             want = O.encode(k, n, data)
-            return desc, np.array_equal(host(out), data) and all(
-                np.array_equal(host(o), w) for o, w in zip(outs, want))
+            enc_ok = all([same(desc, "frag%d" % i, o, w) for i, (o, w) in enumerate(zip(outs, want))])
+            L.decode(CHUNK * nst, m, rows, [outs[x - 1] for x in rows], out)
+            return desc, same(desc, "decoded", out, data) and enc_ok
         if op == "encode_rows":
             m = rng.randrange(1, 1 << n)
             desc["mask"] = m
@@ -136,8 +148,8 @@ def one_call(rng, lists, dev):
             else:
                 L.encode_rows(data.size, src, m, outs)
             want = O.encode(k, n, data)
-            return desc, all(np.array_equal(host(o), want[i]) for i, o in enumerate(outs)
-                             if o is not None)
+            return desc, all([same(desc, "frag%d" % i, o, want[i]) for i, o in enumerate(outs)
+                              if o is not None])
         frags_np = [drng.integers(0, 256, CHUNK * nst, dtype=np.uint8) for _ in range(n)]
         rows = sorted(rng.sample(range(1, n + 1), k))
         mask = sum(1 << (x - 1) for x in rows)
@@ -146,8 +158,8 @@ def one_call(rng, lists, dev):
             fr = [A.buf(frags_np[x - 1]) for x in rows]
             out = A.buf(nbytes=CHUNK * k * nst)
             L.decode_batch(nst, mask, rows, fr, out)
-            return desc, np.array_equal(host(out), O.decode(k, rows, [frags_np[x - 1]
-                                                                      for x in rows]))
+            return desc, same(desc, "decoded", out, O.decode(k, rows, [frags_np[x - 1]
+                                                                         for x in rows]))
         if op == "heal":
             fr = [A.buf(frags_np[x - 1]) for x in rows]
             lost = [b for b in range(n) if not (mask >> b) & 1]
@@ -156,8 +168,8 @@ def one_call(rng, lists, dev):
             outs = [A.buf(nbytes=CHUNK * nst) for _ in tgt]
             L.heal(nst, mask, fr, tmask, outs)
             full = O.encode(k, n, O.decode(k, rows, [frags_np[x - 1] for x in rows]))
-            return desc, all(np.array_equal(host(o), full[b])
-                             for o, b in zip(outs, sorted(tgt)))
+            return desc, all([same(desc, "frag%d" % b, o, full[b])
+                              for o, b in zip(outs, sorted(tgt))])
         if op == "decode_mixed":
             grp = rng.choice([1, 2, 4, 8, 16, 64])
             ng = (nst + grp - 1) // grp
@@ -200,7 +212,7 @@ def one_call(rng, lists, dev):
             L.writev_encode(head, A.buf(user), None if oh is None else A.buf(oh),
                             None if ot is None else A.buf(ot), outs)
         want = O.encode(k, n, O.writev_merge(k, head, user, oh, ot))
-        return desc, all(np.array_equal(host(o), w) for o, w in zip(outs, want))
+        return desc, all([same(desc, "frag%d" % i, o, w) for i, (o, w) in enumerate(zip(outs, want))])
     finally:
         A.free()
 
