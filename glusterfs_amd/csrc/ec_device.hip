@@ -748,6 +748,55 @@ BufPool &buf_pool()
 
 /* ---------------------------------------- deferred host registration (r04) */
 
+/* Ranges registered through ec_method_host_register[_async], page-rounded.
+ * The runtime pins and maps whole pages, so two registrations that share a
+ * page would share its GPU mapping, and unregistering one would unmap a page
+ * the other's kernels still use (tools/fuzz_api.py registered neighbouring
+ * heap arrays this way: a mismatch in r04x, a GPU memory fault in r04z2).
+ * A registration overlapping a live one is refused with -EEXIST instead (the
+ * range stays pageable to the coder, which stages it); GlusterFS's arenas
+ * are page-aligned mmaps and never overlap. */
+class RangeSet {
+  public:
+    /* reserve [p, p + n) rounded out to pages; false if it overlaps */
+    bool reserve(const void *p, size_t n)
+    {
+        const uintptr_t s = (uintptr_t)p & ~kPageMask;
+        const uintptr_t e = ((uintptr_t)p + n + kPageMask) & ~kPageMask;
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = by_start_.lower_bound(s);
+        if (it != by_start_.end() && it->first < e)
+            return false;
+        if (it != by_start_.begin() && std::prev(it)->second.first > s)
+            return false;
+        by_start_[s] = {e, (uintptr_t)p};
+        start_of_[(uintptr_t)p] = s;
+        return true;
+    }
+
+    void release(const void *p)
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        const auto it = start_of_.find((uintptr_t)p);
+        if (it == start_of_.end())
+            return;
+        by_start_.erase(it->second);
+        start_of_.erase(it);
+    }
+
+  private:
+    static constexpr uintptr_t kPageMask = 4095;
+    std::mutex mu_;
+    std::map<uintptr_t, std::pair<uintptr_t, uintptr_t>> by_start_; /* s -> (e, p) */
+    std::map<uintptr_t, uintptr_t> start_of_;                        /* p -> s */
+};
+
+RangeSet &user_ranges()
+{
+    static RangeSet *r = new RangeSet;
+    return *r;
+}
+
 /* ec_method_host_register_async: GlusterFS calls the arena hook from
  * __iobuf_pool_add_arena with iobuf_pool->mutex held (iobuf.c:157), so a
  * hipHostRegister there (hundreds of us for a 2-4 MiB arena, and arenas of
@@ -761,6 +810,8 @@ class RegQueue {
   public:
     int submit(void *p, size_t n)
     {
+        if (!user_ranges().reserve(p, n))
+            return -EEXIST;
         std::lock_guard<std::mutex> g(mu_);
         if (!started_) {
             std::thread([this] { loop(); }).detach();
@@ -779,10 +830,12 @@ class RegQueue {
             for (auto it = q_.begin(); it != q_.end(); ++it)
                 if (it->first == p) {
                     q_.erase(it);
+                    user_ranges().release(p);
                     return 0;
                 }
             done_cv_.wait(g, [&] { return busy_ != p; });
         }
+        user_ranges().release(p);
         const uint64_t t0 = mono_us();
         const hipError_t e = hipHostUnregister(p);
         unreg_us_.fetch_add(mono_us() - t0, std::memory_order_relaxed);
@@ -825,6 +878,7 @@ class RegQueue {
             const uint64_t dt = mono_us() - t0;
             if (e != hipSuccess) {
                 (void)hipGetLastError();
+                user_ranges().release(r.first);
                 if (fails_.fetch_add(1) == 0)
                     fprintf(stderr, "[ec-mi355x] deferred hipHostRegister(%p, %zu) failed: %s; "
                                     "buffers there stay pageable\n",
@@ -1628,8 +1682,13 @@ int ecd_host_register(void *p, size_t bytes)
         return -ENODEV;
     if (!p || bytes == 0)
         return -EINVAL;
+    if (pool_owns(p, 1) || !user_ranges().reserve(p, bytes)) {
+        set_err("hipHostRegister", hipErrorHostMemoryAlreadyRegistered);
+        return -EEXIST;
+    }
     const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped);
     if (e != hipSuccess) {
+        user_ranges().release(p);
         set_err("hipHostRegister", e);
         return e == hipErrorHostMemoryAlreadyRegistered ? -EEXIST : -ENOMEM;
     }
@@ -1651,6 +1710,8 @@ int ecd_host_register_async(void *p, size_t bytes)
         return -ENODEV;
     if (!p || bytes == 0)
         return -EINVAL;
+    if (pool_owns(p, 1))
+        return -EEXIST;
     return reg_queue().submit(p, bytes);
 }
 

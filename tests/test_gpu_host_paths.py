@@ -32,18 +32,21 @@ class Bufs:
     'registered' (pageable pinned through ec_method_host_register)."""
 
     def __init__(self, ec, kind):
-        self.ec, self.kind, self.keep, self.regs = ec, kind, [], []
+        self.ec, self.kind, self.keep, self.regs, self.maps = ec, kind, [], [], []
 
     def new(self, nbytes, fill=None):
         if self.kind == "pageable":
             a = np.empty(nbytes, np.uint8)
         elif self.kind == "registered":
-            a = np.empty(nbytes + 4096, np.uint8)
-            off = (-a.ctypes.data) % 4096
-            a = a[off:off + nbytes]
+            # its own page-aligned mapping, as an iobuf arena: registrations
+            # that share a page are refused (ec_device.hip RangeSet)
+            import mmap
+            m = mmap.mmap(-1, (nbytes + 4095) // 4096 * 4096)
+            a = np.frombuffer(m, np.uint8)[:nbytes]
             r = self.ec.host_registered(a)
             r.__enter__()
             self.regs.append(r)
+            self.maps.append((m, a))
         else:
             extra = 8 if self.kind == "misaligned" else 0
             p = self.ec.PinnedArray(nbytes + extra)
@@ -58,6 +61,7 @@ class Bufs:
             r.__exit__()
         for p in self.keep:
             p.free()
+        self.regs, self.maps = [], []     # the mappings go with their last views
 
 
 KINDS = ["pinned", "pageable", "misaligned", "registered", "mixed"]

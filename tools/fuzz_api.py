@@ -15,8 +15,10 @@ share one kind (mixing host and device is -EINVAL by contract; mixing host
 kinds is what the pool / pinned / pageable draws across calls exercise).
 Prints a progress line every ~10 s and one JSON summary; exit status 1 on
 the first mismatch (its parameters are printed, and FUZZ_SEED replays it).
-EC_GPU_ALWAYS=1 keeps host calls on the GPU.  Usage: python tools/fuzz_api.py"""
+EC_GPU_ALWAYS=1 keeps host calls on the GPU; FUZZ_KINDS restricts the
+buffer kinds.  Usage: python tools/fuzz_api.py"""
 import json
+import mmap
 import os
 import random
 import sys
@@ -51,13 +53,13 @@ class Arena:
             if data is not None:
                 t.copy_(torch.from_numpy(data))
             return t
-        if self.kind == "registered":     # an existing range registered (an iobuf arena)
-            raw = np.empty(n + 8192, np.uint8)
-            a = raw[(-raw.ctypes.data) % 4096:][:n + 4096]
+        if self.kind == "registered":     # an existing mapping registered (an iobuf arena)
+            m = mmap.mmap(-1, (n + 4095) // 4096 * 4096)
+            a = np.frombuffer(m, np.uint8)
             rc = g.ec_method.lib.ec_method_host_register(a.ctypes.data, a.nbytes)
             if rc == 0:
                 self.regs.append(a.ctypes.data)
-            self.keep_raw.append(raw)
+            self.keep_raw.append(m)
             a = a[:n]
             if data is not None:
                 a[:] = data
@@ -107,6 +109,9 @@ def one_call(rng, lists, dev):
     op = rng.choice(OPS)
     kinds = ["device", "device_offset", "pinned", "registered", "pool", "pageable",
              "misaligned"] if dev is not None else ["pool", "pageable"]
+    only = os.environ.get("FUZZ_KINDS")          # e.g. "device_offset registered"
+    if only:
+        kinds = [x for x in kinds if x in only.split()] or kinds
     kind = rng.choice(kinds)
 
     nst = rng.choice([1, 2, 7, 8, 9, 31, 64, 100, 257, 1000, 1031,
