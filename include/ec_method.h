@@ -297,14 +297,17 @@ void *ec_method_host_alloc(size_t bytes);
 void ec_method_host_free(void *p);
 /* Pin and map an existing host range (e.g. a GlusterFS iobuf arena, see
  * INTEGRATION.md) so buffers inside it take the zero-copy path.  Returns 0
- * or -errno.  Unregister before freeing the memory. */
+ * or -errno; -EEXIST for a range sharing a page with a live registration
+ * (or inside the pinned pool): pages are mapped whole, and unregistering one
+ * of two registrations of a page would unmap it under the other.  Unregister
+ * before freeing the memory. */
 int32_t ec_method_host_register(void *p, size_t bytes);
 /* Unregister a range registered by either call below or above (a range still
  * waiting in the deferred queue is dropped; one being registered is waited
  * for).  Returns 0 or -errno. */
 int32_t ec_method_host_unregister(void *p);
 /* Deferred registration: queue the range for a library thread and return at
- * once (0 or -errno).  For callers holding a lock, such as GlusterFS's arena
+ * once (0 or -errno, -EEXIST as above, checked at once).  For callers holding a lock, such as GlusterFS's arena
  * hook, which runs under iobuf_pool->mutex (iobuf.c:157): until the thread has
  * registered the range, buffers in it are coded as pageable memory. */
 int32_t ec_method_host_register_async(void *p, size_t bytes);
