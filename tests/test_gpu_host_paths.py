@@ -205,6 +205,33 @@ def test_decode_16p4_host_kinds(ec, oracle, kind, group):
         p.close()
 
 
+def test_register_overlap_refused(ec):
+    """Two registrations must not share a page (the runtime maps pages
+    whole; unregistering one would unmap the other's): a range overlapping
+    a live one, or inside the pinned pool, is -EEXIST, synchronously for
+    both calls; after the first is unregistered the second goes through."""
+    import errno
+    import mmap
+    lib = ec.ec_method.lib
+    m = mmap.mmap(-1, 16 << 10)
+    a = np.frombuffer(m, np.uint8)
+    base = a.ctypes.data
+    assert lib.ec_method_host_register(base, 8 << 10) == 0
+    try:
+        assert lib.ec_method_host_register(base + (4 << 10), 8 << 10) == -errno.EEXIST
+        assert lib.ec_method_host_register(base + (8 << 10) - 1, 100) == -errno.EEXIST
+        assert lib.ec_method_host_register_async(base + 100, 4 << 10) == -errno.EEXIST
+        pb = ec.PoolBuffer(1 << 20)
+        if pb.pooled:
+            assert lib.ec_method_host_register(pb.array.ctypes.data, 1 << 20) == -errno.EEXIST
+        pb.free()
+    finally:
+        assert lib.ec_method_host_unregister(base) == 0
+    assert lib.ec_method_host_register(base + (4 << 10), 8 << 10) == 0
+    assert lib.ec_method_host_unregister(base + (4 << 10)) == 0
+    del a
+
+
 def test_register_errors(ec):
     import ctypes
     lib = ec.ec_method.lib
