@@ -36,7 +36,7 @@ import oracle as O  # noqa: E402  (the checker)
 
 CHUNK = 512
 GEOS = [(2, 1), (3, 2), (4, 2), (5, 2), (6, 3), (8, 4), (8, 3), (10, 4), (12, 4), (16, 4), (16, 8)]
-OPS = ["encode", "encode_rows", "decode", "decode_mixed", "heal", "writev", "dropin"]
+OPS = ["encode", "encode_rows", "decode", "decode_mixed", "heal", "writev", "dropin", "volume"]
 
 
 class Arena:
@@ -128,6 +128,25 @@ def one_call(rng, lists, dev):
             L.encode_batch(nst, src, outs)
             want = O.encode(k, n, data)
             return desc, all([same(desc, "frag%d" % i, o, w) for i, (o, w) in enumerate(zip(outs, want))])
+        if op == "volume":
+            # a volume brought up and torn down while others code (ec.c:837
+            # init, :198 fini), with a random cpu-extensions value
+            gen = rng.choice(["auto", "hip"] if kind.startswith("device") else
+                             ["auto", "none", "avx", "x64", "hip"])
+            desc["gen"] = gen
+            src = A.buf(data)
+            outs = [A.buf(nbytes=CHUNK * nst) for _ in range(n)]
+            with g.ECMatrixList(k, n, gen=gen) as V:
+                V.encode_batch(nst, src, outs)
+                rows = sorted(rng.sample(range(1, n + 1), k))
+                m = sum(1 << (x - 1) for x in rows)
+                desc["mask"] = m
+                out = A.buf(nbytes=data.size)
+                V.decode_batch(nst, m, rows, [outs[x - 1] for x in rows], out)
+            want = O.encode(k, n, data)
+            return desc, all([same(desc, "frag%d" % i, o, w)
+                              for i, (o, w) in enumerate(zip(outs, want))]) and \
+                same(desc, "decoded", out, data)
         if op == "dropin":
             # the reference's own two calls (ec-method.h:31-46): encode by
             # size, then decode by fragment size from a random brick set
