@@ -5,7 +5,8 @@ tool, GPU box; runs on the CPU engine too).
 For FUZZ_SECS seconds (default 120), FUZZ_THREADS threads (default 8) draw
 random calls -- geometry k+r (k 2..16), size (1 stripe .. ~4 MiB), buffer
 kind (device tensor, device tensor at an odd byte offset, pinned, registered
-range, pool, pageable, misaligned pinned) and entry
+range, pool, pageable, misaligned pinned, or a different host kind per
+buffer of the call, as a patched client's calls are) and entry
 point (encode, encode_rows, decode, decode_mixed, heal, writev_encode, and
 the reference's own size-based encode + decode pair; device buffers go
 through the _device forms where they differ) -- run
@@ -42,10 +43,17 @@ OPS = ["encode", "encode_rows", "decode", "decode_mixed", "heal", "writev", "dro
 class Arena:
     """Buffers of one kind for one call; freed together."""
 
-    def __init__(self, kind, dev):
+    def __init__(self, kind, dev, rng=None):
         self.kind, self.dev, self.keep, self.regs, self.keep_raw = kind, dev, [], [], []
+        self.rng = rng or random.Random(0)
+        self.subs = []
 
     def buf(self, data=None, nbytes=None):
+        if self.kind == "mixed_host":   # every buffer of the call its own host kind
+            sub = Arena(self.rng.choice(["pinned", "registered", "pool", "pageable", "misaligned"]),
+                        self.dev)
+            self.subs.append(sub)
+            return sub.buf(data, nbytes)
         n = data.size if data is not None else nbytes
         if self.kind in ("device", "device_offset"):
             off = 3 if self.kind == "device_offset" else 0   # a tensor slice at an odd byte
@@ -80,6 +88,8 @@ class Arena:
         return a
 
     def free(self):
+        for sub in self.subs:
+            sub.free()
         for p in self.keep:
             p.free()
         for p in self.regs:
@@ -108,7 +118,7 @@ def one_call(rng, lists, dev):
     L = lists[(k, r)]
     op = rng.choice(OPS)
     kinds = ["device", "device_offset", "pinned", "registered", "pool", "pageable",
-             "misaligned"] if dev is not None else ["pool", "pageable"]
+             "misaligned", "mixed_host"] if dev is not None else ["pool", "pageable"]
     only = os.environ.get("FUZZ_KINDS")          # e.g. "device_offset registered"
     if only:
         kinds = [x for x in kinds if x in only.split()] or kinds
@@ -120,7 +130,7 @@ def one_call(rng, lists, dev):
     drng = np.random.default_rng(seed)
     data = drng.integers(0, 256, CHUNK * k * nst, dtype=np.uint8)
     desc = dict(op=op, k=k, n=n, kind=kind, nst=nst, seed=seed)
-    A = Arena(kind, dev)
+    A = Arena(kind, dev, rng)
     try:
         if op == "encode":
             src = A.buf(data)
