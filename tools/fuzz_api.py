@@ -37,7 +37,8 @@ import oracle as O  # noqa: E402  (the checker)
 
 CHUNK = 512
 GEOS = [(2, 1), (3, 2), (4, 2), (5, 2), (6, 3), (8, 4), (8, 3), (10, 4), (12, 4), (16, 4), (16, 8)]
-OPS = ["encode", "encode_rows", "decode", "decode_mixed", "heal", "writev", "dropin", "volume"]
+OPS = ["encode", "encode_rows", "decode", "decode_mixed", "heal", "writev", "dropin", "volume",
+       "stream_chain"]
 
 
 class Arena:
@@ -117,6 +118,8 @@ def one_call(rng, lists, dev):
     n = k + r
     L = lists[(k, r)]
     op = rng.choice(OPS)
+    if op == "stream_chain" and dev is None:
+        op = "encode"                          # device-resident only
     kinds = ["device", "device_offset", "pinned", "registered", "pool", "pageable",
              "misaligned", "mixed_host"] if dev is not None else ["pool", "pageable"]
     only = os.environ.get("FUZZ_KINDS")          # e.g. "device_offset registered"
@@ -138,6 +141,42 @@ def one_call(rng, lists, dev):
             L.encode_batch(nst, src, outs)
             want = O.encode(k, n, data)
             return desc, all([same(desc, "frag%d" % i, o, w) for i, (o, w) in enumerate(zip(outs, want))])
+        if op == "stream_chain":
+            if not kind.startswith("device"):
+                kind = desc["kind"] = "device"
+                A.kind = "device"
+            # device-resident calls queued on a side stream with no sync in
+            # between (stream order is the only ordering): encode, a mixed
+            # decode over up to 40 masks (past the kernel-argument segment:
+            # the device pattern table and its per-stream cache), a heal
+            src = A.buf(data)
+            frags = [A.buf(nbytes=CHUNK * nst) for _ in range(n)]
+            grp = rng.choice([8, 16, 64])
+            ng = (nst + grp - 1) // grp
+            pool = []
+            for _ in range(rng.randint(1, 40)):
+                pool.append(sum(1 << (x - 1) for x in sorted(rng.sample(range(1, n + 1), k))))
+            uniq = sorted(set(pool))
+            ids = torch.tensor([rng.randrange(len(uniq)) for _ in range(ng)], dtype=torch.uint8,
+                               device=dev)
+            out = A.buf(nbytes=data.size)
+            rows = sorted(rng.sample(range(1, n + 1), k))
+            m = sum(1 << (x - 1) for x in rows)
+            lost = [b for b in range(n) if not (m >> b) & 1]
+            tgt = sorted(rng.sample(lost, rng.randint(1, len(lost))))
+            houts = [A.buf(nbytes=CHUNK * nst) for _ in tgt]
+            desc.update(masks=len(uniq), grp=grp, mask=m)
+            st = torch.cuda.Stream(device=dev)
+            st.wait_stream(torch.cuda.current_stream(dev))
+            L.encode_device(dev.index, st.cuda_stream, nst, src, frags)
+            L.decode_mixed_device(dev.index, st.cuda_stream, nst, grp, ids, uniq, frags, out)
+            L.heal_device(dev.index, st.cuda_stream, nst, m, [frags[x - 1] for x in rows],
+                          sum(1 << b for b in tgt), houts)
+            st.synchronize()
+            want = O.encode(k, n, data)
+            return desc, all([same(desc, "frag%d" % i, f, w) for i, (f, w) in enumerate(zip(frags, want))]) \
+                and same(desc, "decoded", out, data) and \
+                all([same(desc, "heal%d" % b, h, want[b]) for h, b in zip(houts, tgt)])
         if op == "volume":
             # a volume brought up and torn down while others code (ec.c:837
             # init, :198 fini), with a random cpu-extensions value
