@@ -16,8 +16,8 @@ share one kind (mixing host and device is -EINVAL by contract; mixing host
 kinds is what the pool / pinned / pageable draws across calls exercise).
 Prints a progress line every ~10 s and one JSON summary; exit status 1 on
 the first mismatch (its parameters are printed, and FUZZ_SEED replays it).
-EC_GPU_ALWAYS=1 keeps host calls on the GPU; FUZZ_KINDS restricts the
-buffer kinds.  Usage: python tools/fuzz_api.py"""
+EC_GPU_ALWAYS=1 keeps host calls on the GPU; FUZZ_KINDS / FUZZ_OPS restrict
+the buffer kinds / entry points.  Usage: python tools/fuzz_api.py"""
 import json
 import mmap
 import os
@@ -117,7 +117,8 @@ def one_call(rng, lists, dev):
     k, r = rng.choice(GEOS)
     n = k + r
     L = lists[(k, r)]
-    op = rng.choice(OPS)
+    ops = [o for o in OPS if o in os.environ.get("FUZZ_OPS", "").split()] or OPS
+    op = rng.choice(ops)
     if op == "stream_chain" and dev is None:
         op = "encode"                          # device-resident only
     kinds = ["device", "device_offset", "pinned", "registered", "pool", "pageable",

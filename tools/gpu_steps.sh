@@ -35,6 +35,7 @@ for step in "$@"; do
     zctpb) run zctpb 900 bash -c 'for r in 1 2; do for c in "0 2048" "4 2048" "0 1024" "0 4096"; do set -- $c; EC_GPU_ALWAYS=1 EC_ZC_TPB=$1 EC_ZC_INFLIGHT_KB=$2 ZC_SIZES="${ZC_SIZES:-1 2 4 8 16 64 256}" python3 tools/zc_sizes.py || exit 1; done; done' ;;
     zcheal) run zcheal 600 bash -c 'for r in 1 2; do for v in 0 1; do EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v ZC_GEOS="16+4 8+4" ZC_SIZES="4 16 64" python3 tools/zc_sizes.py || exit 1; done; done' ;;
     fuzz) run fuzz $(( ${FUZZ_SECS:-150} + 300 )) bash -c 'EC_GPU_ALWAYS=1 FUZZ_SECS=${FUZZ_SECS:-150} python3 -u tools/fuzz_api.py && EC_GPU_ALWAYS=0 FUZZ_SECS=60 python3 -u tools/fuzz_api.py' ;;
+    rmwab) run rmwab 600 bash -c 'export EC_GPU_ALWAYS=1 FUZZ_THREADS=12 FUZZ_SECS=${FUZZ_SECS:-100} FUZZ_KINDS="device device_offset" FUZZ_OPS="writev decode encode stream_chain"; echo "== default (LDS-DMA at the caller alignment)"; python3 -u tools/fuzz_api.py; a=$?; echo "== EC_MI355X_ENC=0 (register encoders, aligned loads + alignbyte)"; EC_MI355X_ENC=0 python3 -u tools/fuzz_api.py; b=$?; echo "rc default=$a enc0=$b"' ;;
     regrepro) run regrepro 600 env EC_GPU_ALWAYS=1 python3 -u tools/reg_repro.py ${REPRO_ITERS:-60} ;;
     pcie) run pcie 200 bash -c 'for m in 4 16 256; do python3 tools/pcie_probe.py $m || exit 1; done' ;;
     hsweep) run hsweep 300 bash -c "cd /tmp && export TMPDIR=/tmp && EC_GPU_ALWAYS=1 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_hsweep_$TAG -o run --output-format csv -- python3 $R/bench.py --heal-sweep gpu --steps 64 && python3 $R/tools/prof_filter.py $R/gpurun_out/prof_hsweep_$TAG ec_ && python3 $R/tools/trace_seq.py $R/gpurun_out/prof_hsweep_$TAG" ;;
