@@ -490,9 +490,14 @@ class PatTableCache {
         std::lock_guard<std::mutex> g(mu_);
         Entry &e = e_[ref.slot];
         hipEvent_t ev = nullptr;
-        for (auto &r : e.readers)
-            if (r.first == s)
-                ev = r.second;
+        /* hipStreamPerThread is one handle for a different stream in every
+         * thread: re-recording one event for it would drop the reads another
+         * thread's stream still has queued, so each of its readers keeps its
+         * own event */
+        if (s != hipStreamPerThread)
+            for (auto &r : e.readers)
+                if (r.first == s)
+                    ev = r.second;
         if (!ev) {
             if (e.readers.size() >= kMaxReaders) {
                 /* many distinct streams: fold the oldest reader into a wait

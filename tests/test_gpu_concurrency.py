@@ -160,3 +160,45 @@ def test_drop_in_encode_advances_pointers_under_concurrency(ec, oracle):
             for i in range(n):
                 assert np.array_equal(frags[i], want[i]), (t, i)
         run_threads(worker, 8)
+
+
+def test_device_tables_on_per_thread_streams(ec, oracle):
+    """Mixed decodes whose patterns need the device table (> 7 masks of
+    16+4), from 8 threads on their per-thread default streams (stream NULL:
+    one handle, a different stream per thread), with more distinct mask
+    sets than the table cache holds, so entries are evicted while other
+    threads' reads may be queued; other threads allocate and free device
+    memory meanwhile.  Every output against the oracle."""
+    import itertools
+    import torch
+    k, n, nst, grp = 16, 20, 96, 8
+    allm = [sum(1 << b for b in c) for c in itertools.combinations(range(n), k)]
+    rng0 = np.random.default_rng(5)
+    sets = [sorted(int(x) for x in rng0.choice(allm, 10, replace=False)) for _ in range(40)]
+    data = rand_bytes(CHUNK * k * nst, seed=123)
+    enc = oracle.encode(k, n, data)
+    frags = [torch.from_numpy(f).cuda() for f in enc]
+    torch.cuda.synchronize()
+    L = ec.ECMatrixList(k, n)
+
+    def worker(t):
+        rng = np.random.default_rng(t)
+        for it in range(12):
+            if t % 4 == 3:            # allocation churn beside the decodes
+                x = torch.empty((1 << 20) + int(rng.integers(0, 4096)), dtype=torch.uint8,
+                                device="cuda").fill_(t)
+                del x
+                continue
+            masks = sets[int(rng.integers(0, len(sets)))]
+            ids = torch.tensor(rng.integers(0, len(masks), nst // grp), dtype=torch.uint8,
+                               device="cuda")
+            torch.cuda.synchronize()
+            out = torch.empty(CHUNK * k * nst, dtype=torch.uint8, device="cuda")
+            L.decode_mixed_device(0, None, nst, grp, ids, masks, frags, out)
+            ec.sync_device(0)
+            assert np.array_equal(out.cpu().numpy(), data), (t, it)
+
+    try:
+        run_threads(worker, 8)
+    finally:
+        L.fini()
