@@ -49,7 +49,13 @@ typedef struct ecd_combine_desc {
 /* Number of usable gfx950 devices (0 when none: the host layer then codes
  * with its CPU engine, ec_cpu.h). */
 int ecd_device_count(void);
+/* The calling thread's last failure ("" if none; on a node without a device,
+ * why).  ecd_error_seq counts the failures the thread has recorded, so a
+ * caller can tell whether a failing call said why; ecd_set_error records a
+ * failure of the host layer (argument errors and the like). */
 const char *ecd_last_error(void);
+uint64_t ecd_error_seq(void);
+void ecd_set_error(const char *text);
 
 /* ---- device-pointer entry points: asynchronous on `stream` (NULL = the
  * calling thread's per-thread default stream of `device`); 0 or -errno. */

@@ -35,6 +35,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -85,13 +86,36 @@ int copy_threads()
     return v;
 }
 
-std::mutex g_err_mu;
-std::string g_err;
+/* Error text of the last failure, per calling thread (ec_method_last_error):
+ * a GlusterFS client codes on several epoll threads and the heal syncenv, so
+ * a process-wide slot handed one thread's failure to another's log line (r04:
+ * a combine's -EIO reported a much earlier test's hipHostUnregister text).
+ * t_err_seq counts the failures this thread recorded, so ec_method.c can tell
+ * whether a failing call already said why. */
+thread_local std::string t_err;
+thread_local uint64_t t_err_seq = 0;
+/* set once by discover(): the reason a node has no usable device */
+std::string g_discover_err;
+
+void set_err_text(std::string s)
+{
+    t_err = std::move(s);
+    ++t_err_seq;
+}
 
 void set_err(const char *what, hipError_t e)
 {
-    std::lock_guard<std::mutex> g(g_err_mu);
-    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    set_err_text(std::string(what) + ": " + hipGetErrorString(e) + " (" +
+                 std::to_string((int)e) + ")");
+}
+
+/* A HIP error the thread left pending before this call (the caller's own
+ * unchecked call, or one the runtime records without failing the call) is
+ * not this call's: drop it, so the launch checks below -- hipGetLastError
+ * after each launch -- see only the launch. */
+inline void clear_stale_error()
+{
+    (void)hipGetLastError();
 }
 
 #define HIPCHK(call)                                                           \
@@ -165,10 +189,8 @@ void discover()
         g_dev_ids[g_ndev++] = i;
     }
     host_devices_from_env();
-    if (g_ndev == 0) {
-        std::lock_guard<std::mutex> g(g_err_mu);
-        g_err = "no gfx950 (MI355X) device visible";
-    }
+    if (g_ndev == 0)
+        g_discover_err = "no gfx950 (MI355X) device visible";
 }
 
 hipStream_t pick_stream(void *stream)
@@ -192,8 +214,9 @@ class DeviceGuard {
     ~DeviceGuard()
     {
         int cur = -1;
-        if (prev_ >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev_)
-            (void)hipSetDevice(prev_);
+        if (prev_ >= 0 && (hipGetDevice(&cur) != hipSuccess ||
+                           (cur != prev_ && hipSetDevice(prev_) != hipSuccess)))
+            (void)hipGetLastError();
     }
     DeviceGuard(const DeviceGuard &) = delete;
     DeviceGuard &operator=(const DeviceGuard &) = delete;
@@ -614,6 +637,14 @@ class BufPool {
         return off % cs + n <= cs;
     }
 
+    /* [p, p + n) touches the pool's reserved range (registered or not) */
+    bool overlaps(const void *p, size_t n) const
+    {
+        const uint8_t *b = base_.load(std::memory_order_acquire);
+        const uintptr_t q = (uintptr_t)p;
+        return b && q < (uintptr_t)b + span_ && q + n > (uintptr_t)b;
+    }
+
     void stats(ecd_pool_stats_t *s) const
     {
         s->pool_bytes = grown_.load() * kGran;
@@ -774,14 +805,28 @@ class RangeSet {
         return true;
     }
 
-    void release(const void *p)
+    /* Drop the reservation of p.  Returns false when p's registration had
+     * failed (mark_failed): the owner's unregister must then not call
+     * hipHostUnregister, which could unmap another caller's registration
+     * at the same start address. */
+    bool release(const void *p)
     {
         std::lock_guard<std::mutex> g(mu_);
         const auto it = start_of_.find((uintptr_t)p);
         if (it == start_of_.end())
-            return;
+            return true;
         by_start_.erase(it->second);
         start_of_.erase(it);
+        return failed_.erase((uintptr_t)p) == 0;
+    }
+
+    /* A deferred registration of p failed: the range stays reserved (so no
+     * other registration can take its pages) until its owner unregisters. */
+    void mark_failed(const void *p)
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        if (start_of_.count((uintptr_t)p))
+            failed_.insert((uintptr_t)p);
     }
 
   private:
@@ -789,6 +834,7 @@ class RangeSet {
     std::mutex mu_;
     std::map<uintptr_t, std::pair<uintptr_t, uintptr_t>> by_start_; /* s -> (e, p) */
     std::map<uintptr_t, uintptr_t> start_of_;                        /* p -> s */
+    std::set<uintptr_t> failed_;                                     /* p       */
 };
 
 RangeSet &user_ranges()
@@ -835,7 +881,8 @@ class RegQueue {
                 }
             done_cv_.wait(g, [&] { return busy_ != p; });
         }
-        user_ranges().release(p);
+        if (!user_ranges().release(p))
+            return 0;      /* its deferred registration failed: nothing mapped */
         const uint64_t t0 = mono_us();
         const hipError_t e = hipHostUnregister(p);
         unreg_us_.fetch_add(mono_us() - t0, std::memory_order_relaxed);
@@ -878,7 +925,7 @@ class RegQueue {
             const uint64_t dt = mono_us() - t0;
             if (e != hipSuccess) {
                 (void)hipGetLastError();
-                user_ranges().release(r.first);
+                user_ranges().mark_failed(r.first);
                 if (fails_.fetch_add(1) == 0)
                     fprintf(stderr, "[ec-mi355x] deferred hipHostRegister(%p, %zu) failed: %s; "
                                     "buffers there stay pageable\n",
@@ -912,6 +959,14 @@ bool pool_owns(const void *p, size_t n)
     return buf_pool().owns(p, n);
 }
 
+/* a caller registration that would overlap the pool's range: refused (the
+ * pool's slabs are registered already, and the rest of its range is
+ * reserved for them) */
+bool pool_overlaps(const void *p, size_t n)
+{
+    return buf_pool().overlaps(p, n);
+}
+
 /* Per-device pipeline resources (pooled). */
 constexpr int kSlots = 2;
 
@@ -942,8 +997,7 @@ int grow(uint8_t *(&slot)[kSlots], size_t &cap, size_t want, int dev)
     for (auto &p : slot) {
         p = static_cast<uint8_t *>(pinned_alloc(want, device_numa(dev)));
         if (!p) {
-            std::lock_guard<std::mutex> g(g_err_mu);
-            g_err = "pinned staging allocation failed";
+            set_err_text("pinned staging allocation of " + std::to_string(want) + " bytes failed");
             return -ENOMEM;
         }
     }
@@ -970,7 +1024,7 @@ Stage *acquire(int dev)
         ok = hipEventCreateWithFlags(&s->done[i], hipEventDisableTiming | hipEventBlockingSync) ==
              hipSuccess;
     if (!ok) {
-        (void)hipGetLastError();
+        set_err("staging stream / event creation", hipGetLastError());
         delete s;
         return nullptr;
     }
@@ -1104,6 +1158,7 @@ int run_encode_dev(int dev, const EncodeJob &j)
     if (j.s1 <= j.s0)
         return 0;
     DeviceGuard dg;
+    clear_stale_error();
     HIPCHK(hipSetDevice(g_dev_ids[dev]));
     const uint64_t stripe_in = (uint64_t)j.k * ECD_CHUNK, cnt_all = j.s1 - j.s0;
     const bool in_direct =
@@ -1166,6 +1221,7 @@ int run_decode_dev(int dev, const DecodeJob &j)
     if (j.s1 <= j.s0)
         return 0;
     DeviceGuard dg;
+    clear_stale_error();
     HIPCHK(hipSetDevice(g_dev_ids[dev]));
     const uint64_t out_stripe = (uint64_t)j.rows * ECD_CHUNK, cnt_all = j.s1 - j.s0;
     bool in_direct[ECD_MAX_ROWS] = {}, out_direct[ECD_MAX_ROWS] = {}, all_direct = true;
@@ -1309,8 +1365,7 @@ bool take_injected_fault()
     while (v > 0 && !g_inject_faults.compare_exchange_weak(v, v - 1))
         ;
     if (v > 0) {
-        std::lock_guard<std::mutex> g(g_err_mu);
-        g_err = "injected device fault (ec_method_inject_device_faults)";
+        set_err_text("injected device fault (ec_method_inject_device_faults)");
         return true;
     }
     return false;
@@ -1341,6 +1396,7 @@ int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
     if ((uint64_t)ndev > units)
         ndev = (int)std::max<uint64_t>(1, units);
     std::vector<int> rcs(ndev, 0);
+    std::vector<std::string> errs(ndev);   /* a worker's failure, for the caller */
     std::vector<uint64_t> share(ndev, 0);
     std::vector<std::thread> th;
     for (int d = 0; d < ndev; ++d) {
@@ -1352,15 +1408,23 @@ int partition(int ndev, uint64_t nstripes, uint64_t align, uint64_t bytes, F fn)
         if (d == ndev - 1)
             rcs[d] = fn(dev, s0, s1);
         else
-            th.emplace_back([&, d, dev, s0, s1] { rcs[d] = fn(dev, s0, s1); });
+            th.emplace_back([&, d, dev, s0, s1] {
+                const uint64_t seq = t_err_seq;
+                rcs[d] = fn(dev, s0, s1);
+                if (rcs[d] && t_err_seq != seq)
+                    errs[d] = t_err;
+            });
     }
     for (auto &t : th)
         t.join();
     for (int d = 0; d < ndev; ++d)
         g_inflight[g_host_devs[d]].fetch_sub(share[d]);
-    for (int rc : rcs)
-        if (rc)
-            return rc;
+    for (int d = 0; d < ndev; ++d)
+        if (rcs[d]) {
+            if (!errs[d].empty())
+                set_err_text("device " + std::to_string(g_host_devs[d]) + ": " + errs[d]);
+            return rcs[d];
+        }
     return 0;
 }
 
@@ -1376,10 +1440,25 @@ int ecd_device_count(void)
 
 const char *ecd_last_error(void)
 {
-    static thread_local std::string copy;
-    std::lock_guard<std::mutex> g(g_err_mu);
-    copy = g_err;
-    return copy.c_str();
+    if (t_err.empty() && g_ndev == 0)
+        return g_discover_err.c_str();   /* written once, before any call returns */
+    return t_err.c_str();
+}
+
+uint64_t ecd_error_seq(void)
+{
+    return t_err_seq;
+}
+
+void ecd_set_error(const char *text)
+{
+    set_err_text(text ? text : "");
+}
+
+int ecd_hip_fail(const char *what, int hip_error)
+{
+    set_err(what, (hipError_t)hip_error);
+    return -EIO;
 }
 
 int ecd_has_vander(uint32_t k, uint32_t n)
@@ -1393,6 +1472,7 @@ int ecd_encode_vander(int device, void *stream, uint32_t k, uint32_t n, uint64_t
     if (ecd_device_count() <= device || device < 0)
         return -ENODEV;
     DeviceGuard dg;
+    clear_stale_error();
     HIPCHK(hipSetDevice(g_dev_ids[device]));
     return ecdk_encode_vander(pick_stream(stream), k, n, nstripes, in, out);
 }
@@ -1402,6 +1482,7 @@ int ecd_combine(int device, void *stream, const ecd_combine_desc_t *d)
     if (ecd_device_count() <= device || device < 0)
         return -ENODEV;
     DeviceGuard dg;
+    clear_stale_error();
     HIPCHK(hipSetDevice(g_dev_ids[device]));
     return ecdk_combine(pick_stream(stream), d);
 }
@@ -1490,6 +1571,7 @@ int ecd_writev_encode_device(int device, void *stream, uint32_t k, uint32_t n, u
         ts += b2 - (nst - 1) * S; /* ec_merge_stripe_tail_locked, :1898-1908 */
     }
     DeviceGuard dg;
+    clear_stale_error();
     HIPCHK(hipSetDevice(g_dev_ids[device]));
     hipStream_t st = pick_stream(stream);
     const bool fused = ecdk_has_vander(k, n);
@@ -1682,7 +1764,7 @@ int ecd_host_register(void *p, size_t bytes)
         return -ENODEV;
     if (!p || bytes == 0)
         return -EINVAL;
-    if (pool_owns(p, 1) || !user_ranges().reserve(p, bytes)) {
+    if (pool_overlaps(p, bytes) || !user_ranges().reserve(p, bytes)) {
         set_err("hipHostRegister", hipErrorHostMemoryAlreadyRegistered);
         return -EEXIST;
     }
@@ -1710,8 +1792,10 @@ int ecd_host_register_async(void *p, size_t bytes)
         return -ENODEV;
     if (!p || bytes == 0)
         return -EINVAL;
-    if (pool_owns(p, 1))
+    if (pool_overlaps(p, bytes)) {
+        set_err("hipHostRegister (deferred)", hipErrorHostMemoryAlreadyRegistered);
         return -EEXIST;
+    }
     return reg_queue().submit(p, bytes);
 }
 

@@ -7,6 +7,10 @@
 
 #include "ec_device.h"
 
+/* Record `what` failed with HIP error `hip_error` as the calling thread's
+ * last error (ec_device.hip); returns -EIO. */
+extern "C" int ecd_hip_fail(const char *what, int hip_error);
+
 int ecdk_has_vander(uint32_t k, uint32_t n);
 /* zc: buffers are pinned host memory coded over PCIe (ec_encode_vander_zc) */
 int ecdk_encode_vander(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes,

@@ -52,6 +52,24 @@ int ecdk_ldsnt_override = [] {
 
 namespace {
 
+/* Status of the launch just issued on this thread: the entry points clear
+ * any stale error first (ec_device.hip clear_stale_error), so a failure here
+ * is the launch's, and it is recorded under the kernel's name. */
+int launch_ok(const char *what)
+{
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : ecd_hip_fail(what, e);
+}
+
+/* Check a HIP call whose failure fails the call: recorded, -EIO. */
+int hip_ok(hipError_t e, const char *what)
+{
+    if (e == hipSuccess)
+        return 0;
+    (void)hipGetLastError();
+    return ecd_hip_fail(what, e);
+}
+
 /* Non-temporal staging loads for a call that reads more than 256 MiB, the
  * MALL's capacity: none of its input can still be cached when the same data
  * comes round again, and default-policy allocation only costs.  Below that,
@@ -91,15 +109,15 @@ int ensure_lds_limit(const void *kern, int bytes)
     static std::mutex mu;
     static std::vector<std::pair<const void *, int>> done;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess)
-        return -EIO;
+    if (int rc = hip_ok(hipGetDevice(&dev), "hipGetDevice"))
+        return rc;
     std::lock_guard<std::mutex> g(mu);
     for (const auto &e : done)
         if (e.first == kern && e.second == dev)
             return 0;
-    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) !=
-        hipSuccess)
-        return -EIO;
+    if (int rc = hip_ok(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes),
+                        "hipFuncSetAttribute(MaxDynamicSharedMemorySize)"))
+        return rc;
     done.emplace_back(kern, dev);
     return 0;
 }
@@ -113,7 +131,7 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
     if (zc && vander_use_zc<W>(nstripes)) {
         hipLaunchKernelGGL((ec_encode_vander_zc<K, N, W>), dim3((u32)kZcBlocks), dim3(kBlock), 0,
                            s, static_cast<const uint8_t *>(in), f, nstripes);
-        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+        return launch_ok("launch_vander");
     }
     const uint64_t g = vander_grid<W>(nstripes);
     if (g == 0)
@@ -122,7 +140,7 @@ int launch_vander(hipStream_t s, uint64_t nstripes, const void *in, void *const 
         return -EINVAL;
     hipLaunchKernelGGL((ec_encode_vander<K, N, W, NTS>), dim3((u32)g), dim3(kBlock), 0, s,
                        static_cast<const uint8_t *>(in), f, nstripes);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("launch_vander");
 }
 
 /* The 8-stripe ec_combine (k > 8): single pattern, mixed patterns (kernel
@@ -152,7 +170,7 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
         hipLaunchKernelGGL((ec_combine<K, 1, NW, false, NTS, 2, false, true, 1, false, 1, LA>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("launch_combine");
 }
 
 } // namespace
@@ -193,7 +211,7 @@ int launch_encode_narrow(hipStream_t s, uint64_t nstripes, EncSrc src, void *con
         return -EINVAL;
     hipLaunchKernelGGL((ec_encode_tile_t<K, N, 4, NW, true, DIRECT, true, SM, LA>), dim3((u32)g),
                        dim3(NW * 64), (encode_tile_t_lds<4, NW, true>(K)), s, src, f, nstripes);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("launch_encode_narrow");
 }
 
 /* Row-group encoder (ec_encode_tile_rb): 4-stripe tiles, RB rows per wave,
@@ -212,7 +230,7 @@ int launch_encode_rb(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *
     hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true, SM, LA>), dim3((u32)g),
                        dim3((N / RB) * 64), (encode_tile_rb_lds<N, 4, RB, true>(K)), s, src, f,
                        nstripes);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("launch_encode_rb");
 }
 
 /* The shipped tile encoder of a geometry (4+2, 8+4, 16+4), -ENOTSUP else. */
@@ -286,7 +304,7 @@ int ecdk_rmw_gather(hipStream_t s, const uint8_t *head, const uint8_t *user, con
         return -EINVAL;
     RmwSrc v{head, user, tail, b1, b2};
     hipLaunchKernelGGL(ec_rmw_gather, dim3((u32)g), dim3(kBlock), 0, s, v, o0, n, dst);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("ecdk_rmw_gather");
 }
 
 template <int K, int N, int W, int LM>
@@ -303,7 +321,7 @@ int launch_vander_rmw(hipStream_t s, uint64_t nstripes, const uint8_t *edge,
         return -EINVAL;
     hipLaunchKernelGGL((ec_encode_vander_rmw<K, N, W, LM>), dim3((u32)g), dim3(kBlock), 0, s, edge,
                        user_shift, f, nstripes);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("launch_vander_rmw");
 }
 
 /* LM = 1: dword-aligned loads + v_alignbyte for the interior stripes.
@@ -378,7 +396,7 @@ int enqueue_upload(hipStream_t s, const std::vector<u32> &w, u32 *tab)
         memcpy(c.w, w.data() + o, (size_t)c.n * 4);
         hipLaunchKernelGGL(ec_pat_upload, dim3(1), dim3(256), 0, s, c);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("enqueue_upload");
 }
 
 /* Mixed calls whose patterns exceed the 2 KiB argument space read their
@@ -387,11 +405,29 @@ int enqueue_upload(hipStream_t s, const std::vector<u32> &w, u32 *tab)
  * device (per device, LRU): a repeated call skips the allocation and the
  * upload launches (one per 2 KiB: ~9 for 64 masks of 16+4, ~50 us of
  * stream time per call).  An entry is reused only for identical words, and
- * evicted (LRU) only when no call holds it.  Every stream that launched a
- * reader records the entry's event for that stream at release(); eviction
- * waits on those events with the cache lock dropped (the slot is marked
- * busy meanwhile), so one caller's eviction never blocks other callers or
- * waits for unrelated work on the device. */
+ * evicted (LRU) only when no call holds it.
+ *
+ * Ordering is all on the device; no call waits on the host (r05):
+ *   - a table is uploaded on the stream of the call that missed, which
+ *     records the entry's `ready` event; a call that hits makes its stream
+ *     wait for `ready`;
+ *   - every stream that read the table records its own reader event at
+ *     release(); a reader is a (stream, thread) pair, because
+ *     hipStreamPerThread is one handle for a different stream in every
+ *     thread, and re-recording a reader's event for its next call is exact
+ *     (one in-order stream);
+ *   - eviction makes the evicting call's stream wait for every reader event,
+ *     then frees the old table and allocates the new one stream-ordered
+ *     (hipFreeAsync / hipMallocAsync) on that stream, so the memory is reused
+ *     only after every read of it;
+ *   - the reader list stays bounded without a wait: entries whose event has
+ *     completed are dropped, and past kMaxReaders live readers the oldest is
+ *     folded into the releasing stream (it waits for that event, so the
+ *     event it records next covers both).
+ * r04 waited on the host instead (hipEventSynchronize + hipFree with the
+ * lock dropped at eviction, hipEventSynchronize under the lock at the fold)
+ * and ignored those calls' errors; one of them failed under the 4-thread
+ * evict/hit/upload test on a fresh box and surfaced as a launch -EIO. */
 class PatTableCache {
   public:
     struct Ref {
@@ -410,21 +446,25 @@ class PatTableCache {
         if (off)
             return -EBUSY;
         int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess)
-            return -EIO;
+        if (int rc = hip_ok(hipGetDevice(&dev), "hipGetDevice"))
+            return rc;
         uint64_t h = 1469598103934665603ull;     /* FNV-1a over the words */
         for (u32 x : w)
             h = (h ^ x) * 1099511628211ull;
-        std::unique_lock<std::mutex> g(mu_);
+        std::lock_guard<std::mutex> g(mu_);
         int victim = -1;
         for (int i = 0; i < kEntries; ++i) {
             Entry &e = e_[i];
             if (e.ptr && e.dev == dev && e.hash == h && e.words == w) {
+                if (int rc = hip_ok(hipStreamWaitEvent(s, e.ready, 0),
+                                    "hipStreamWaitEvent(pattern table ready)"))
+                    return rc;
                 ++e.inflight;
                 e.tick = ++tick_;
                 ref.slot = i;
                 ref.ptr = e.ptr;
-                return hipStreamWaitEvent(s, e.ready, 0) == hipSuccess ? 0 : -EIO;
+                ++hits_;
+                return 0;
             }
             if (e.inflight == 0 && (e.dev == dev || !e.ptr) &&
                 (victim < 0 || !e.ptr || (e_[victim].ptr && e.tick < e_[victim].tick)))
@@ -433,108 +473,161 @@ class PatTableCache {
         if (victim < 0)
             return -EBUSY;                    /* every entry in use: per call */
         Entry &e = e_[victim];
-        e.inflight = 1;                       /* ours: nobody else picks it */
-        e.hash = 0;
-        e.words.clear();
         if (e.ptr) {
-            /* evict: wait for the streams that read it, without the lock */
-            std::vector<hipEvent_t> wait;
-            for (auto &r : e.readers)
-                wait.push_back(r.second);
-            u32 *old = e.ptr;
+            /* evict: s waits for every reader, then frees the old table */
+            for (const Reader &r : e.readers)
+                if (int rc = hip_ok(hipStreamWaitEvent(s, r.ev, 0),
+                                    "hipStreamWaitEvent(pattern table reader)"))
+                    return rc;                /* entry left as it was */
+            if (int rc = hip_ok(hipFreeAsync(e.ptr, s), "hipFreeAsync(pattern table)"))
+                return rc;
             e.ptr = nullptr;
-            g.unlock();
-            for (hipEvent_t ev : wait)
-                (void)hipEventSynchronize(ev);
-            (void)hipFree(old);
-            g.lock();
+            e.hash = 0;
+            e.words.clear();
+            drop_readers(e);                  /* their reads are waited for by s */
+            ++evictions_;
         }
-        if (e.dev != dev) {
-            for (auto &r : e.readers)
-                (void)hipEventDestroy(r.second);
-            e.readers.clear();
+        if (e.dev != dev) {                   /* an empty entry moves device */
+            drop_readers(e);
             if (e.ready)
                 (void)hipEventDestroy(e.ready);
+            (void)hipGetLastError();
             e.ready = nullptr;
-            if (hipEventCreateWithFlags(&e.ready, hipEventDisableTiming) != hipSuccess) {
-                (void)hipGetLastError();
-                e.inflight = 0;
-                return -EIO;
+            e.dev = -1;
+            if (int rc = hip_ok(hipEventCreateWithFlags(&e.ready, hipEventDisableTiming),
+                                "hipEventCreate(pattern table)")) {
+                e.ready = nullptr;
+                return rc;
             }
             e.dev = dev;
         }
-        if (hipMalloc(reinterpret_cast<void **>(&e.ptr), w.size() * 4) != hipSuccess) {
+        u32 *p = nullptr;
+        if (hipMallocAsync(reinterpret_cast<void **>(&p), w.size() * 4, s) != hipSuccess) {
             (void)hipGetLastError();
-            e.ptr = nullptr;
-            e.inflight = 0;
-            return -ENOMEM;
+            return -EBUSY;                    /* the per-call table says why */
         }
-        if (enqueue_upload(s, w, e.ptr) != 0 || hipEventRecord(e.ready, s) != hipSuccess) {
-            (void)hipStreamSynchronize(s);
-            (void)hipFree(e.ptr);
-            e.ptr = nullptr;
-            e.inflight = 0;
-            return -EIO;
+        int rc = enqueue_upload(s, w, p);
+        if (rc == 0)
+            rc = hip_ok(hipEventRecord(e.ready, s), "hipEventRecord(pattern table ready)");
+        if (rc) {
+            (void)hipFreeAsync(p, s);
+            (void)hipGetLastError();
+            return rc;
         }
+        e.ptr = p;
         e.hash = h;
         e.words = w;
         e.tick = ++tick_;
+        e.inflight = 1;
         ref.slot = victim;
-        ref.ptr = e.ptr;
+        ref.ptr = p;
+        ++uploads_;
         return 0;
     }
 
-    /* The work that reads the table has been enqueued on `s`. */
-    void release(const Ref &ref, hipStream_t s)
+    /* The work that reads the table has been enqueued on `s`.  0, or the
+     * error that made release() drain `s` instead of tracking it. */
+    int release(const Ref &ref, hipStream_t s)
+    {
+        const uint64_t tok = s == hipStreamPerThread ? thread_token() : 0;
+        int rc = 0;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            Entry &e = e_[ref.slot];
+            hipEvent_t ev = nullptr;
+            for (const Reader &r : e.readers)
+                if (r.s == s && r.tok == tok)
+                    ev = r.ev;
+            if (!ev) {
+                prune_readers(e, s);
+                if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess)
+                    e.readers.push_back({s, tok, ev});
+                else
+                    rc = hip_ok(hipGetLastError(), "hipEventCreate(pattern table reader)"), ev = nullptr;
+            }
+            if (ev && hipEventRecord(ev, s) != hipSuccess)
+                rc = hip_ok(hipGetLastError(), "hipEventRecord(pattern table reader)");
+            --e.inflight;
+        }
+        if (rc)                                /* untracked: drain the stream */
+            (void)hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize");
+        return rc;
+    }
+
+    void stats(uint64_t *hits, uint64_t *uploads, uint64_t *evictions, uint64_t *folds)
     {
         std::lock_guard<std::mutex> g(mu_);
-        Entry &e = e_[ref.slot];
-        hipEvent_t ev = nullptr;
-        /* hipStreamPerThread is one handle for a different stream in every
-         * thread: re-recording one event for it would drop the reads another
-         * thread's stream still has queued, so each of its readers keeps its
-         * own event */
-        if (s != hipStreamPerThread)
-            for (auto &r : e.readers)
-                if (r.first == s)
-                    ev = r.second;
-        if (!ev) {
-            if (e.readers.size() >= kMaxReaders) {
-                /* many distinct streams: fold the oldest reader into a wait
-                 * now (rare; keeps the list bounded) */
-                (void)hipEventSynchronize(e.readers.front().second);
-                (void)hipEventDestroy(e.readers.front().second);
-                e.readers.erase(e.readers.begin());
-            }
-            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess)
-                e.readers.emplace_back(s, ev);
-            else {
-                (void)hipGetLastError();
-                ev = nullptr;
-            }
-        }
-        if (!ev || hipEventRecord(ev, s) != hipSuccess) {
-            (void)hipGetLastError();
-            (void)hipStreamSynchronize(s);  /* cannot track it: drain it */
-        }
-        --e.inflight;
+        *hits = hits_;
+        *uploads = uploads_;
+        *evictions = evictions_;
+        *folds = folds_;
     }
 
   private:
+    struct Reader {
+        hipStream_t s;
+        uint64_t tok;        /* thread token for hipStreamPerThread, else 0 */
+        hipEvent_t ev;
+    };
     struct Entry {
         int dev = -1;
         uint64_t hash = 0, tick = 0;
         std::vector<u32> words;
         u32 *ptr = nullptr;
         hipEvent_t ready = nullptr;           /* the upload has landed */
-        std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
+        std::vector<Reader> readers;
         int inflight = 0;
     };
+
+    /* a token per thread, never reused (a thread id can be) */
+    static uint64_t thread_token()
+    {
+        static std::atomic<uint64_t> next{1};
+        static thread_local const uint64_t tok = next.fetch_add(1);
+        return tok;
+    }
+
+    /* events may be destroyed with work pending on them: the runtime frees
+     * them once the work completes, and waits already enqueued still hold */
+    static void drop_readers(Entry &e)
+    {
+        for (const Reader &r : e.readers)
+            (void)hipEventDestroy(r.ev);
+        e.readers.clear();
+        (void)hipGetLastError();
+    }
+
+    /* Make room for a new reader without a host wait: drop readers whose
+     * reads have completed; if kMaxReaders are still live, `s` waits for the
+     * oldest, whose reads the event `s` records next then covers. */
+    void prune_readers(Entry &e, hipStream_t s)
+    {
+        if (e.readers.size() < kMaxReaders)
+            return;
+        size_t o = 0;
+        for (size_t i = 0; i < e.readers.size(); ++i) {
+            const hipError_t q = hipEventQuery(e.readers[i].ev);
+            if (q == hipSuccess)
+                (void)hipEventDestroy(e.readers[i].ev);
+            else
+                e.readers[o++] = e.readers[i];
+        }
+        e.readers.resize(o);
+        (void)hipGetLastError();              /* hipErrorNotReady is no error */
+        if (e.readers.size() >= kMaxReaders &&
+            hipStreamWaitEvent(s, e.readers.front().ev, 0) == hipSuccess) {
+            (void)hipEventDestroy(e.readers.front().ev);
+            e.readers.erase(e.readers.begin());
+            ++folds_;
+        }
+        (void)hipGetLastError();
+    }
+
     static constexpr int kEntries = 16;
     static constexpr size_t kMaxReaders = 16;
     std::mutex mu_;
     Entry e_[kEntries];
-    uint64_t tick_ = 0;
+    uint64_t tick_ = 0, hits_ = 0, uploads_ = 0, evictions_ = 0, folds_ = 0;
 };
 
 /* never destroyed: tables and events would be freed after the runtime */
@@ -559,9 +652,9 @@ int upload_table(hipStream_t s, const ecd_combine_desc_t *d, CombineArgs &a, u32
     }
     if (rc != -EBUSY)
         return rc;
-    if (hipMallocAsync(reinterpret_cast<void **>(tab), nw * 4, s) != hipSuccess) {
+    if (const hipError_t e = hipMallocAsync(reinterpret_cast<void **>(tab), nw * 4, s)) {
         *tab = nullptr;
-        (void)hipGetLastError();
+        (void)hip_ok(e, "hipMallocAsync(per-call pattern table)");
         return -ENOMEM;
     }
     a.patg = *tab;
@@ -580,8 +673,8 @@ int sorted_slots(hipStream_t s, const CombineArgs &a0, F tiles)
     const uint64_t nslots_max = a0.nstripes + 8ull * a0.npatterns;
     u32 *ws = nullptr;
     const size_t bytes = (size_t)(512 + 1 + nslots_max) * 4;
-    if (hipMallocAsync(reinterpret_cast<void **>(&ws), bytes, s) != hipSuccess) {
-        (void)hipGetLastError();
+    if (const hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&ws), bytes, s)) {
+        (void)hip_ok(e, "hipMallocAsync(slot workspace)");
         return -ENOMEM;
     }
     u32 *counts = ws, *cursors = ws + 256, *total = ws + 512, *slots = ws + 513;
@@ -590,20 +683,20 @@ int sorted_slots(hipStream_t s, const CombineArgs &a0, F tiles)
     a.slot_count = total;
     const uint64_t nb = (a.nstripes + kSlotBlock * kSlotPerThread - 1) / (kSlotBlock * kSlotPerThread);
     int rc = 0;
-    if (hipMemsetAsync(counts, 0, 256 * 4, s) != hipSuccess ||
-        hipMemsetAsync(slots, 0xFF, nslots_max * 4, s) != hipSuccess)
-        rc = -EIO;
+    rc = hip_ok(hipMemsetAsync(counts, 0, 256 * 4, s), "hipMemsetAsync(slot counts)");
+    if (rc == 0)
+        rc = hip_ok(hipMemsetAsync(slots, 0xFF, nslots_max * 4, s), "hipMemsetAsync(slots)");
     if (rc == 0) {
         hipLaunchKernelGGL(ec_slots_count, dim3((u32)nb), dim3(kSlotBlock), 0, s, a, counts);
         hipLaunchKernelGGL(ec_slots_scan, dim3(1), dim3(256), 0, s, counts, cursors, total);
         hipLaunchKernelGGL(ec_slots_scatter, dim3((u32)nb), dim3(kSlotBlock), 0, s, a, cursors,
                            slots);
-        rc = hipGetLastError() == hipSuccess ? 0 : -EIO;
+        rc = launch_ok("sorted_slots");
     }
     if (rc == 0)
         rc = tiles(s, a);
-    (void)hipFreeAsync(ws, s);
-    return rc;
+    const int frc = hip_ok(hipFreeAsync(ws, s), "hipFreeAsync(slot workspace)");
+    return rc ? rc : frc;
 }
 
 /* ------------------------------------------------ narrow tiles (r03) */
@@ -618,7 +711,7 @@ int launch_n1(hipStream_t s, const CombineArgs &a, uint64_t g)
     const size_t lds = combine_n_lds<NW, WOT, PG>((int)a.k);
     hipLaunchKernelGGL((ec_combine_n<K, NW, MIXED, NTS, WOT, PG, SL, 1, LA>), dim3((u32)g),
                        dim3(NW * 64), lds, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("launch_n1");
 }
 
 /* one k-bucket: single pattern, mixed, device pattern table, sorted slots */
@@ -686,9 +779,11 @@ int combine_any(hipStream_t s, const ecd_combine_desc_t *d)
             rc = launch_combine_k<NTS, kLdsDmaDefault>(s, a);
     }
     if (ref.slot >= 0)
-        pat_tables().release(ref, s);
-    if (tab)
-        (void)hipFreeAsync(tab, s);
+        (void)pat_tables().release(ref, s);   /* a failure drained s: the call stands */
+    if (tab) {
+        const int frc = hip_ok(hipFreeAsync(tab, s), "hipFreeAsync(per-call pattern table)");
+        rc = rc ? rc : frc;
+    }
     return rc;
 }
 
@@ -839,9 +934,8 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
             ensure_lds_limit(kern, (int)((128u << 10) + 8 * ECD_MAX_ROWS)) != 0)
             return -EIO;
         void *args[] = {&a};
-        if (hipLaunchKernel(kern, dim3((u32)gdb), dim3(NW * 64), args, lds_db4, s) != hipSuccess)
-            return -EIO;
-        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+        return hip_ok(hipLaunchKernel(kern, dim3((u32)gdb), dim3(NW * 64), args, lds_db4, s),
+                      "hipLaunchKernel(ec_combine_zc_db)");
     }
     if (zc_double_buffered() &&
         ((d->k <= 8 && lds_db <= (128u << 10) + 8 * ECD_MAX_ROWS) || db16)) {
@@ -867,9 +961,8 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
             ensure_lds_limit(kern, db16 ? (int)kLdsPerCu : (int)((128u << 10) + 8 * ECD_MAX_ROWS)) != 0)
             return -EIO;
         void *args[] = {&a};
-        if (hipLaunchKernel(kern, dim3((u32)gdb), dim3(NW * 64), args, lds_db, s) != hipSuccess)
-            return -EIO;
-        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+        return hip_ok(hipLaunchKernel(kern, dim3((u32)gdb), dim3(NW * 64), args, lds_db, s),
+                      "hipLaunchKernel(ec_combine_zc_db)");
     }
     if (d->k <= 4) {
         if (a.group_pattern)
@@ -893,5 +986,5 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
         else
             hipLaunchKernelGGL((ec_combine_zc<16, NW, false>), dim3((u32)g), dim3(NW * 64), lds, s, a);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    return launch_ok("ecdk_combine_host");
 }

@@ -569,10 +569,21 @@ ec_method_xover_observe(int32_t engine, int32_t op, uint32_t k, uint64_t user, u
     return 0;
 }
 
+/* Field by field with atomic stores: obs_record / obs_explore update the
+ * same fields atomically from coding threads, so a reset during traffic is
+ * not a data race (a memset was, under TSan).  A call in flight may still
+ * add its sample after the reset. */
 void
 ec_method_xover_reset(void)
 {
-    memset(ecm_obs, 0, sizeof(ecm_obs));
+    ecm_obs_t *o = &ecm_obs[0][0][0][0];
+    size_t i;
+
+    for (i = 0; i < sizeof(ecm_obs) / sizeof(ecm_obs[0][0][0][0]); i++) {
+        __atomic_store_n(&o[i].kbps, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&o[i].lost, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&o[i].n, 0, __ATOMIC_RELAXED);
+    }
 }
 
 /* bytes of the n buffers b[0..n) (len bytes each; NULL entries skipped) that
@@ -605,6 +616,8 @@ gpu_failed(int rc)
                 ecd_last_error());
     return 1;
 }
+
+static int32_t ecm_ret(const char *fn, uint64_t seq, int32_t rc);
 
 #define CTX(list) ((ecm_ctx_t *)(list)->code)
 #define LRU_HEAD(list) ((ecm_matrix_t *)(void *)(list)->lru)
@@ -903,20 +916,20 @@ ec_method_host_free(void *p)
     ecd_host_free(p);
 }
 
-int32_t
-ec_method_host_register(void *p, size_t bytes)
+static int32_t
+ecm_host_register_impl(void *p, size_t bytes)
 {
     return ecd_host_register(p, bytes);
 }
 
-int32_t
-ec_method_host_unregister(void *p)
+static int32_t
+ecm_host_unregister_impl(void *p)
 {
     return ecd_host_unregister(p);
 }
 
-int32_t
-ec_method_host_register_async(void *p, size_t bytes)
+static int32_t
+ecm_host_register_async_impl(void *p, size_t bytes)
 {
     return ecd_host_register_async(p, bytes);
 }
@@ -1001,9 +1014,9 @@ pick_engine(ecm_ctx_t *ctx, const char *gen)
         snprintf(ctx->engine_name, sizeof(ctx->engine_name), "cpu/%s", ecc_isa_name(ctx->isa));
 }
 
-int32_t
-ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t rows,
-               uint32_t max, const char *gen)
+static int32_t
+ecm_init_impl(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t rows,
+             uint32_t max, const char *gen)
 {
     ecm_ctx_t *ctx;
     uint32_t i;
@@ -1082,8 +1095,8 @@ ec_method_fini(ec_matrix_list_t *list)
     memset(list, 0, sizeof(*list));
 }
 
-int32_t
-ec_method_update(xlator_t *xl, ec_matrix_list_t *list, const char *gen)
+static int32_t
+ecm_update_impl(xlator_t *xl, ec_matrix_list_t *list, const char *gen)
 {
     (void)xl;
     (void)list;
@@ -1269,6 +1282,7 @@ void
 ec_method_encode(ec_matrix_list_t *list, uint64_t size, void *in, void **out)
 {
     ecm_ctx_t *ctx = CTX(list);
+    uint64_t seq;
     uint32_t i;
     int rc;
 
@@ -1280,8 +1294,10 @@ ec_method_encode(ec_matrix_list_t *list, uint64_t size, void *in, void **out)
     /* host buffers cannot fail here (a device error is redone on the CPU
      * engine); what is left is a caller error or a fault of caller-provided
      * device memory, which no fallback can read */
+    seq = ecd_error_seq();
     rc = encode_any(list, size / list->stripe, in, out);
     if (rc != 0) {
+        ecm_ret("ec_method_encode", seq, rc);
         ecm_log("ec_method_encode failed (%d): %s", rc, ecd_last_error());
         abort(); /* the reference's encode cannot fail; never return bad data */
     }
@@ -1289,9 +1305,9 @@ ec_method_encode(ec_matrix_list_t *list, uint64_t size, void *in, void **out)
         out[i] = (uint8_t *)out[i] + size / list->columns;
 }
 
-int32_t
-ec_method_encode_batch(ec_matrix_list_t *list, uint64_t nstripes, const void *in,
-                       void *const *out)
+static int32_t
+ecm_encode_batch_impl(ec_matrix_list_t *list, uint64_t nstripes, const void *in,
+                     void *const *out)
 {
     if (!list || !CTX(list) || (!in && nstripes) || (!out && nstripes))
         return -EINVAL;
@@ -1420,10 +1436,10 @@ encode_rows_any(ec_matrix_list_t *list, uint64_t nstripes, const void *in, uintp
     return rc ? rc : ecd_sync(dev, NULL);
 }
 
-int32_t
-ec_method_encode_rows_device(ec_matrix_list_t *list, int device, void *stream,
-                             uint64_t nstripes, const void *in, uintptr_t row_mask,
-                             void *const *out)
+static int32_t
+ecm_encode_rows_device_impl(ec_matrix_list_t *list, int device, void *stream,
+                           uint64_t nstripes, const void *in, uintptr_t row_mask,
+                           void *const *out)
 {
     uint8_t pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K];
     void *outs[ECM_MAX_N];
@@ -1445,6 +1461,7 @@ ec_method_encode_rows(ec_matrix_list_t *list, uint64_t size, void *in, uintptr_t
                       void **out)
 {
     ecm_ctx_t *ctx = CTX(list);
+    uint64_t seq;
     uint32_t i;
     int rc;
 
@@ -1459,8 +1476,10 @@ ec_method_encode_rows(ec_matrix_list_t *list, uint64_t size, void *in, uintptr_t
     }
     if (row_mask == 0)
         return; /* no fragment wanted */
+    seq = ecd_error_seq();
     rc = encode_rows_any(list, size / list->stripe, in, row_mask, out);
     if (rc != 0) {
+        ecm_ret("ec_method_encode_rows", seq, rc);
         ecm_log("ec_method_encode_rows(mask 0x%llx) failed (%d): %s",
                 (unsigned long long)row_mask, rc, ecd_last_error());
         abort(); /* as ec_method_encode: never return bad data */
@@ -1514,9 +1533,9 @@ decode_any(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask, const uint
     return host_decode(ctx, k, k, nstripes, k, in, out, NULL, 1, pat, NULL, 0);
 }
 
-int32_t
-ec_method_decode(ec_matrix_list_t *list, uint64_t size, uintptr_t mask, uint32_t *rows,
-                 void **in, void *out)
+static int32_t
+ecm_decode_impl(ec_matrix_list_t *list, uint64_t size, uintptr_t mask, uint32_t *rows,
+               void **in, void *out)
 {
     if (!list || !CTX(list) || size % EC_METHOD_CHUNK_SIZE != 0 || !rows || !in ||
         (!out && size))
@@ -1525,9 +1544,9 @@ ec_method_decode(ec_matrix_list_t *list, uint64_t size, uintptr_t mask, uint32_t
                       (const void *const *)in, out);
 }
 
-int32_t
-ec_method_decode_batch(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
-                       const uint32_t *rows, const void *const *in, void *out)
+static int32_t
+ecm_decode_batch_impl(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
+                     const uint32_t *rows, const void *const *in, void *out)
 {
     if (!list || !CTX(list) || !rows || !in || (!out && nstripes))
         return -EINVAL;
@@ -1570,9 +1589,9 @@ mask_frags_ok(const ec_matrix_list_t *list, uintptr_t mask, const void *const *f
     return 1;
 }
 
-int32_t
-ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_stripes,
-                       const uintptr_t *group_masks, const void *const *frags, void *out)
+static int32_t
+ecm_decode_mixed_impl(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_stripes,
+                     const uintptr_t *group_masks, const void *const *frags, void *out)
 {
     uint8_t *pats;
     uintptr_t uniq[ECD_MAX_PATTERNS];
@@ -1664,9 +1683,9 @@ heal_pattern(ec_matrix_list_t *list, uintptr_t mask, const uint32_t *rows,
     return 0;
 }
 
-int32_t
-ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
-               const void *const *in, uintptr_t target_mask, void *const *out)
+static int32_t
+ecm_heal_impl(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
+             const void *const *in, uintptr_t target_mask, void *const *out)
 {
     uint8_t pat[ECM_MAX_K + ECM_MAX_N * ECM_MAX_K];
     uint32_t rows[ECM_MAX_K], nt = 0, p;
@@ -1701,10 +1720,10 @@ ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
 
 /* ------------------------------------------------- partial-stripe writes */
 
-int32_t
-ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iovec *iov,
-                        int count, const void *old_head, const void *old_tail,
-                        void *const *out)
+static int32_t
+ecm_writev_encode_impl(ec_matrix_list_t *list, uint64_t head, const struct iovec *iov,
+                      int count, const void *old_head, const void *old_tail,
+                      void *const *out)
 {
     ecm_ctx_t *ctx;
     const void *segp[3 + 64];
@@ -1783,10 +1802,10 @@ ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iove
     return c;
 }
 
-int32_t
-ec_method_writev_encode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t head,
-                               uint64_t size, const void *user, const void *old_head,
-                               const void *old_tail, void *const *out)
+static int32_t
+ecm_writev_encode_device_impl(ec_matrix_list_t *list, int device, void *stream, uint64_t head,
+                             uint64_t size, const void *user, const void *old_head,
+                             const void *old_tail, void *const *out)
 {
     ecm_ctx_t *ctx;
 
@@ -1811,9 +1830,9 @@ desc_init(ecd_combine_desc_t *d, uint32_t k, uint32_t rows, uint64_t nstripes)
     d->pat_bytes = k + rows * k;
 }
 
-int32_t
-ec_method_encode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
-                        const void *in, void *const *out)
+static int32_t
+ecm_encode_device_impl(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                      const void *in, void *const *out)
 {
     ecm_ctx_t *ctx;
     ecd_combine_desc_t d;
@@ -1836,9 +1855,9 @@ ec_method_encode_device(ec_matrix_list_t *list, int device, void *stream, uint64
     return ecd_combine(device, stream, &d);
 }
 
-int32_t
-ec_method_decode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
-                        uintptr_t mask, const void *const *in, void *out)
+static int32_t
+ecm_decode_device_impl(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                      uintptr_t mask, const void *const *in, void *out)
 {
     uint32_t rows[ECM_MAX_K], k, p, r;
     uint8_t src[ECM_MAX_K];
@@ -1870,11 +1889,11 @@ ec_method_decode_device(ec_matrix_list_t *list, int device, void *stream, uint64
     return ecd_combine(device, stream, &d);
 }
 
-int32_t
-ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
-                              uint64_t nstripes, uint64_t group_stripes,
-                              const uint8_t *group_pattern, uint32_t nmasks,
-                              const uintptr_t *masks, const void *const *frags, void *out)
+static int32_t
+ecm_decode_mixed_device_impl(ec_matrix_list_t *list, int device, void *stream,
+                            uint64_t nstripes, uint64_t group_stripes,
+                            const uint8_t *group_pattern, uint32_t nmasks,
+                            const uintptr_t *masks, const void *const *frags, void *out)
 {
     ecd_combine_desc_t d;
     uint32_t k, r, u, shift = 0;
@@ -1922,10 +1941,10 @@ ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
     return rc;
 }
 
-int32_t
-ec_method_heal_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
-                      uintptr_t mask, const void *const *in, uintptr_t target_mask,
-                      void *const *out)
+static int32_t
+ecm_heal_device_impl(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                    uintptr_t mask, const void *const *in, uintptr_t target_mask,
+                    void *const *out)
 {
     uint32_t rows[ECM_MAX_K], nt = 0, p;
     ecd_combine_desc_t d;
@@ -1956,8 +1975,193 @@ ec_method_heal_device(ec_matrix_list_t *list, int device, void *stream, uint64_t
     return ecd_combine(device, stream, &d);
 }
 
+static int32_t
+ecm_sync_device_impl(int device, void *stream)
+{
+    return ecd_sync(device, stream);
+}
+
+/* ------------------------------------------- per-thread error reporting */
+
+/* Every entry point that fails leaves the calling thread a reason in
+ * ec_method_last_error(): the device layer records what failed (the HIP call
+ * or kernel and its error); a failure it did not record -- an argument
+ * error, a geometry the call does not take -- is recorded here as the entry
+ * point and its errno, so a client's log line (ec.c / ec-heal.c callers,
+ * many epoll threads) never shows another call's text. */
+static int32_t
+ecm_ret(const char *fn, uint64_t seq, int32_t rc)
+{
+    char buf[192];
+
+    if (rc < 0 && ecd_error_seq() == seq) {
+        snprintf(buf, sizeof buf, "%s: %s (%d)", fn, strerror(-rc), (int)rc);
+        ecd_set_error(buf);
+    }
+    return rc;
+}
+
+int32_t
+ec_method_init(xlator_t *xl, ec_matrix_list_t *list, uint32_t columns, uint32_t rows,
+               uint32_t max, const char *gen)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_init", seq,
+                   ecm_init_impl(xl, list, columns, rows, max, gen));
+}
+
+int32_t
+ec_method_update(xlator_t *xl, ec_matrix_list_t *list, const char *gen)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_update", seq,
+                   ecm_update_impl(xl, list, gen));
+}
+
+int32_t
+ec_method_encode_batch(ec_matrix_list_t *list, uint64_t nstripes, const void *in,
+                       void *const *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_encode_batch", seq,
+                   ecm_encode_batch_impl(list, nstripes, in, out));
+}
+
+int32_t
+ec_method_encode_rows_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                             const void *in, uintptr_t row_mask, void *const *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_encode_rows_device", seq,
+                   ecm_encode_rows_device_impl(list, device, stream, nstripes, in, row_mask,
+                                               out));
+}
+
+int32_t
+ec_method_decode(ec_matrix_list_t *list, uint64_t size, uintptr_t mask, uint32_t *rows,
+                 void **in, void *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_decode", seq,
+                   ecm_decode_impl(list, size, mask, rows, in, out));
+}
+
+int32_t
+ec_method_decode_batch(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask,
+                       const uint32_t *rows, const void *const *in, void *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_decode_batch", seq,
+                   ecm_decode_batch_impl(list, nstripes, mask, rows, in, out));
+}
+
+int32_t
+ec_method_decode_mixed(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_stripes,
+                       const uintptr_t *group_masks, const void *const *frags, void *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_decode_mixed", seq,
+                   ecm_decode_mixed_impl(list, nstripes, group_stripes, group_masks, frags, out));
+}
+
+int32_t
+ec_method_heal(ec_matrix_list_t *list, uint64_t nstripes, uintptr_t mask, const void *const *in,
+               uintptr_t target_mask, void *const *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_heal", seq,
+                   ecm_heal_impl(list, nstripes, mask, in, target_mask, out));
+}
+
+int32_t
+ec_method_writev_encode(ec_matrix_list_t *list, uint64_t head, const struct iovec *iov,
+                        int count, const void *old_head, const void *old_tail, void *const *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_writev_encode", seq,
+                   ecm_writev_encode_impl(list, head, iov, count, old_head, old_tail, out));
+}
+
+int32_t
+ec_method_writev_encode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t head,
+                               uint64_t size, const void *user, const void *old_head,
+                               const void *old_tail, void *const *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_writev_encode_device", seq,
+                   ecm_writev_encode_device_impl(list, device, stream, head, size, user, old_head,
+                                                 old_tail, out));
+}
+
+int32_t
+ec_method_encode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                        const void *in, void *const *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_encode_device", seq,
+                   ecm_encode_device_impl(list, device, stream, nstripes, in, out));
+}
+
+int32_t
+ec_method_decode_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                        uintptr_t mask, const void *const *in, void *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_decode_device", seq,
+                   ecm_decode_device_impl(list, device, stream, nstripes, mask, in, out));
+}
+
+int32_t
+ec_method_decode_mixed_device(ec_matrix_list_t *list, int device, void *stream,
+                              uint64_t nstripes, uint64_t group_stripes,
+                              const uint8_t *group_pattern, uint32_t nmasks,
+                              const uintptr_t *masks, const void *const *frags, void *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_decode_mixed_device", seq,
+                   ecm_decode_mixed_device_impl(list, device, stream, nstripes, group_stripes,
+                                                group_pattern, nmasks, masks, frags, out));
+}
+
+int32_t
+ec_method_heal_device(ec_matrix_list_t *list, int device, void *stream, uint64_t nstripes,
+                      uintptr_t mask, const void *const *in, uintptr_t target_mask,
+                      void *const *out)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_heal_device", seq,
+                   ecm_heal_device_impl(list, device, stream, nstripes, mask, in, target_mask,
+                                        out));
+}
+
 int32_t
 ec_method_sync_device(int device, void *stream)
 {
-    return ecd_sync(device, stream);
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_sync_device", seq,
+                   ecm_sync_device_impl(device, stream));
+}
+
+int32_t
+ec_method_host_register(void *p, size_t bytes)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_host_register", seq,
+                   ecm_host_register_impl(p, bytes));
+}
+
+int32_t
+ec_method_host_unregister(void *p)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_host_unregister", seq,
+                   ecm_host_unregister_impl(p));
+}
+
+int32_t
+ec_method_host_register_async(void *p, size_t bytes)
+{
+    const uint64_t seq = ecd_error_seq();
+    return ecm_ret("ec_method_host_register_async", seq,
+                   ecm_host_register_async_impl(p, bytes));
 }

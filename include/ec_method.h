@@ -286,7 +286,13 @@ void ec_method_get_stats(ec_method_stats_t *stats);
  * host-buffer device submissions fail with -EIO before touching a device,
  * so the CPU fallback runs. */
 void ec_method_inject_device_faults(uint32_t count);
-/* Last device-layer error string (diagnostics). */
+/* Why the calling thread's last failing call failed (diagnostics): the
+ * device layer's record (the HIP call or kernel and its error), or the
+ * entry point and errno of a failure it did not record (an argument error).
+ * Per thread: a client's epoll threads each read their own.  The text stays
+ * until the thread's next failure ("" if it never failed; on a node without
+ * a device, why none was used).  The pointer is valid until that thread's
+ * next call into the library. */
 const char *ec_method_last_error(void);
 /* Pinned, device-mapped host memory.  Host buffers in such memory (16-byte
  * aligned) are coded in place by the GPU over PCIe with no staging copy;

@@ -1,6 +1,7 @@
 /* Device layer stand-in for the host-only sanitizer build
  * (tests/test_sanitizers.py): no GPU, so ec_method.c takes its CPU engine
  * paths.  Every entry point of glusterfs_amd/csrc/ec_device.h. */
+#include <stdio.h>
 #include <errno.h>
 #include <stddef.h>
 #include <string.h>
@@ -8,7 +9,16 @@
 #include "../../glusterfs_amd/csrc/ec_device.h"
 
 int ecd_device_count(void) { return 0; }
-const char *ecd_last_error(void) { return "no device (sanitizer build)"; }
+/* per-thread error record, as ec_device.hip keeps it */
+static __thread char t_err[256];
+static __thread uint64_t t_seq;
+const char *ecd_last_error(void) { return t_err[0] ? t_err : "no device (sanitizer build)"; }
+uint64_t ecd_error_seq(void) { return t_seq; }
+void ecd_set_error(const char *text)
+{
+    snprintf(t_err, sizeof t_err, "%s", text ? text : "");
+    t_seq++;
+}
 int ecd_has_vander(uint32_t k, uint32_t n) { (void)k; (void)n; return 0; }
 int ecd_encode_vander(int d, void *s, uint32_t k, uint32_t n, uint64_t ns, const void *in,
                       void *const *out)

@@ -139,6 +139,10 @@ def test_patched_iobuf_data_allocator_covers_every_size_class(scratch):
     std = _c_body(io, "iobuf_get_from_stdalloc")
     a, c = std.index("data_alloc((page_size + GF_IOBUF_ALIGN_SIZE) - 1)"), std.index("GF_CALLOC(\n")
     assert a < c
+    # ... and its memory is zeroed, as GF_CALLOC's is (fuse,
+    # protocol/client and other users of > 1 MiB iobufs get calloc'd memory)
+    z = std.index("memset(iobuf->free_ptr, 0, (page_size + GF_IOBUF_ALIGN_SIZE) - 1);")
+    assert a < z < c
     # every free of a non-arena iobuf asks the free hook before GF_FREE
     fr = _c_body(io, "__iobuf_free")
     assert fr.index("data_free(iobuf->free_ptr)") < fr.index("GF_FREE(iobuf->free_ptr)")
