@@ -1589,15 +1589,126 @@ mask_frags_ok(const ec_matrix_list_t *list, uintptr_t mask, const void *const *f
     return 1;
 }
 
+/* Per-thread memo of the packed pattern sets of the last mixed calls (r05).
+ * A self-heal sweep passes the same mask set call after call, and a set
+ * larger than the decode-matrix cache (2 x nodes entries, as ec.c sizes it)
+ * cycles through its LRU, so every call re-inverted every mask: 64 masks of
+ * 16+4 cost ~170 us of host time per call (tools/patcache_threads.py: a
+ * 4 MiB device heal window took ~190 us, ~23 us with one mask).  Keyed by
+ * the volume's serial and the exact mask list; the returned patterns are
+ * valid until this thread's next call of pattern_set. */
+#define ECM_SETMEMO 2
+typedef struct {
+    uint64_t serial, hash;
+    uint32_t nmasks;
+    uintptr_t *masks;
+    uint8_t *pats;
+    size_t cap_masks, cap_pats; /* entries of masks[], bytes of pats[] */
+} ecm_setmemo_t;
+
+typedef struct {
+    ecm_setmemo_t e[ECM_SETMEMO];
+    unsigned next;
+} ecm_setmemos_t;
+
+static pthread_key_t ecm_setmemo_key;
+static pthread_once_t ecm_setmemo_once = PTHREAD_ONCE_INIT;
+static int ecm_setmemo_ok;
+
+static void
+setmemo_free(void *v)
+{
+    ecm_setmemos_t *s = (ecm_setmemos_t *)v;
+    unsigned i;
+
+    for (i = 0; i < ECM_SETMEMO; i++) {
+        free(s->e[i].masks);
+        free(s->e[i].pats);
+    }
+    free(s);
+}
+
+static void
+setmemo_init(void)
+{
+    ecm_setmemo_ok = pthread_key_create(&ecm_setmemo_key, setmemo_free) == 0;
+}
+
+/* The packed patterns (k + k*k bytes each, in `masks` order) of a mask set;
+ * NULL with *rc set on a bad mask or no memory. */
+static const uint8_t *
+pattern_set(ec_matrix_list_t *list, const uintptr_t *masks, uint32_t nmasks, int *rc)
+{
+    ecm_ctx_t *ctx = (ecm_ctx_t *)list->code;
+    const size_t pb = (size_t)list->columns * (1 + list->columns);
+    ecm_setmemos_t *s;
+    ecm_setmemo_t *e;
+    uint64_t h = 1469598103934665603ull; /* FNV-1a */
+    uint32_t u;
+    unsigned i;
+
+    for (u = 0; u < nmasks; u++)
+        h = (h ^ (uint64_t)masks[u]) * 1099511628211ull;
+    pthread_once(&ecm_setmemo_once, setmemo_init);
+    s = ecm_setmemo_ok ? (ecm_setmemos_t *)pthread_getspecific(ecm_setmemo_key) : NULL;
+    if (!s && ecm_setmemo_ok) {
+        s = (ecm_setmemos_t *)calloc(1, sizeof(*s));
+        if (s && pthread_setspecific(ecm_setmemo_key, s) != 0) {
+            free(s);
+            s = NULL;
+        }
+    }
+    if (!s) {
+        *rc = -ENOMEM;
+        return NULL;
+    }
+    for (i = 0; i < ECM_SETMEMO; i++) {
+        e = &s->e[i];
+        if (e->serial == ctx->serial && e->nmasks == nmasks && e->hash == h &&
+            memcmp(e->masks, masks, nmasks * sizeof(*masks)) == 0)
+            return e->pats;
+    }
+    e = &s->e[s->next++ % ECM_SETMEMO];
+    e->serial = 0;
+    if (e->cap_masks < nmasks) {   /* (volumes of any k share the entries) */
+        uintptr_t *m = (uintptr_t *)realloc(e->masks, nmasks * sizeof(*masks));
+
+        if (!m) {
+            *rc = -ENOMEM;
+            return NULL;
+        }
+        e->masks = m;
+        e->cap_masks = nmasks;
+    }
+    if (e->cap_pats < nmasks * pb) {
+        uint8_t *p = (uint8_t *)realloc(e->pats, nmasks * pb);
+
+        if (!p) {
+            *rc = -ENOMEM;
+            return NULL;
+        }
+        e->pats = p;
+        e->cap_pats = nmasks * pb;
+    }
+    for (u = 0; u < nmasks; u++)
+        if ((*rc = mask_pattern(list, masks[u], e->pats + u * pb)) != 0)
+            return NULL;
+    memcpy(e->masks, masks, nmasks * sizeof(*masks));
+    e->nmasks = nmasks;
+    e->hash = h;
+    e->serial = ctx->serial;
+    return e->pats;
+}
+
 static int32_t
 ecm_decode_mixed_impl(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_stripes,
                      const uintptr_t *group_masks, const void *const *frags, void *out)
 {
-    uint8_t *pats;
+    const uint8_t *pats;
     uintptr_t uniq[ECD_MAX_PATTERNS];
     uint8_t *gp;
     uint64_t g, ngroups;
-    uint32_t shift = 0, nu = 0, u, k, pb;
+    uint32_t shift = 0, nu = 0, u, k;
     int rc;
 
     if (!list || !CTX(list) || !group_masks || !frags || (!out && nstripes))
@@ -1609,15 +1720,10 @@ ecm_decode_mixed_impl(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_
     if (nstripes == 0)
         return 0;
     k = list->columns;
-    pb = k + k * k;
     ngroups = (nstripes + group_stripes - 1) / group_stripes;
     gp = (uint8_t *)malloc(ngroups);
-    pats = (uint8_t *)malloc((size_t)ECD_MAX_PATTERNS * pb);
-    if (!gp || !pats) {
-        free(gp);
-        free(pats);
+    if (!gp)
         return -ENOMEM;
-    }
     rc = 0;
     for (g = 0; g < ngroups && rc == 0; g++) {
         for (u = 0; u < nu; u++)
@@ -1632,17 +1738,18 @@ ecm_decode_mixed_impl(ec_matrix_list_t *list, uint64_t nstripes, uint64_t group_
                 rc = -EINVAL;
                 break;
             }
-            rc = mask_pattern(list, group_masks[g], pats + nu * pb);
             uniq[nu++] = group_masks[g];
         }
         gp[g] = (uint8_t)u;
     }
+    pats = NULL;
+    if (rc == 0)
+        pats = pattern_set(list, uniq, nu, &rc);
     if (rc == 0 && (!bufs_on(frags, list->rows, -1) || ecd_ptr_device(out) >= 0))
         rc = -EINVAL; /* host entry point: device buffers go to _device */
     if (rc == 0)
         rc = host_decode(CTX(list), k, k, nstripes, list->rows, frags, out, NULL, nu, pats, gp,
                          shift);
-    free(pats);
     free(gp);
     return rc;
 }
@@ -1897,7 +2004,7 @@ ecm_decode_mixed_device_impl(ec_matrix_list_t *list, int device, void *stream,
 {
     ecd_combine_desc_t d;
     uint32_t k, r, u, shift = 0;
-    uint8_t *ext;
+    const uint8_t *pats;
     int rc;
 
     if (!list || !CTX(list) || !group_pattern || !masks || !frags || !out || nmasks == 0)
@@ -1919,26 +2026,23 @@ ecm_decode_mixed_device_impl(ec_matrix_list_t *list, int device, void *stream,
         d.in_base[u] = frags[u];
     for (r = 0; r < k; r++)
         d.out_base[r] = (uint8_t *)out + (uint64_t)r * EC_METHOD_CHUNK_SIZE;
-    /* more masks than the kernel-argument space holds: the launcher moves
-     * them to a device table (ec_kernels.hip upload_table) */
-    ext = NULL;
-    if ((uint64_t)nmasks * d.pat_bytes > ECD_MAX_PAT_BYTES) {
-        ext = (uint8_t *)malloc((size_t)nmasks * d.pat_bytes);
-        if (!ext)
-            return -ENOMEM;
-        d.pat_ext = ext;
-    }
     rc = 0;
     for (u = 0; u < nmasks && rc == 0; u++)
-        rc = mask_frags_ok(list, masks[u], frags)
-                 ? mask_pattern(list, masks[u], (ext ? ext : d.pat) + u * d.pat_bytes)
-                 : -EINVAL;
+        if (!mask_frags_ok(list, masks[u], frags))
+            rc = -EINVAL;
+    pats = rc == 0 ? pattern_set(list, masks, nmasks, &rc) : NULL;
+    if (rc)
+        return rc;
+    /* more masks than the kernel-argument space holds: the launcher moves
+     * them to a device table (ec_kernels.hip upload_table), reading them
+     * during the call */
+    if ((uint64_t)nmasks * d.pat_bytes > ECD_MAX_PAT_BYTES)
+        d.pat_ext = pats;
+    else
+        memcpy(d.pat, pats, (size_t)nmasks * d.pat_bytes);
     d.group_pattern = group_pattern;
     d.group_shift = shift;
-    if (rc == 0)
-        rc = ecd_combine(device, stream, &d);
-    free(ext);   /* packed into kernel arguments / uploaded during the call */
-    return rc;
+    return ecd_combine(device, stream, &d);
 }
 
 static int32_t

@@ -13,10 +13,45 @@
 #include "ec_method.h"
 
 enum { K = 4, N = 6, NST = 37, THREADS = 8, ITERS = 60 };
+enum { K2 = 16, N2 = 20, NST2 = 16 };
 
-static ec_matrix_list_t list;
+static ec_matrix_list_t list, list16;
 static unsigned char data[512 * K * NST], *frag[N];
+static unsigned char data16[512 * K2 * NST2], *frag16[N2];
 static int failures;
+
+/* Mixed decodes on either volume (r05: the per-thread pattern-set memo is
+ * shared by volumes of different k, and grows as sets grow): a set of 1-12
+ * masks, drawn from a few fixed sets so calls repeat, one mask per stripe
+ * group; every group checked against the data. */
+static void
+mixed(unsigned *seed, int wide)
+{
+    const uint32_t k = wide ? K2 : K, n = wide ? N2 : N, nst = wide ? NST2 : NST;
+    const unsigned char *ref = wide ? data16 : data;
+    unsigned char **fr = wide ? frag16 : frag;
+    const uint32_t group = wide ? 2 : 4, ng = (nst + group - 1) / group;
+    uintptr_t gm[64];
+    unsigned char *out = malloc((size_t)512 * k * nst);
+    unsigned set = rand_r(seed) % 3, sseed = set * 977u + (unsigned)wide;
+    uint32_t nm = 1 + (set * 5 + (unsigned)wide) % 12, g;
+    uintptr_t pool[12];
+
+    for (uint32_t i = 0; i < nm; i++) {
+        uintptr_t m = 0;
+        while ((uint32_t)__builtin_popcountll(m) < k)
+            m |= (uintptr_t)1 << (rand_r(&sseed) % n);
+        pool[i] = m;
+    }
+    for (g = 0; g < ng; g++)
+        gm[g] = pool[rand_r(seed) % nm];
+    memset(out, 0, (size_t)512 * k * nst);
+    if (ec_method_decode_mixed(wide ? &list16 : &list, nst, group, gm,
+                               (const void *const *)fr, out) != 0 ||
+        memcmp(out, ref, (size_t)512 * k * nst) != 0)
+        __atomic_add_fetch(&failures, 1, __ATOMIC_RELAXED);
+    free(out);
+}
 
 static void *
 worker(void *arg)
@@ -37,6 +72,7 @@ worker(void *arg)
         if (ec_method_decode(&list, 512 * NST, m, rows, in, out) != 0 ||
             memcmp(out, data, sizeof(data)) != 0)
             __atomic_add_fetch(&failures, 1, __ATOMIC_RELAXED);
+        mixed(&seed, it & 1);
         if (it % 10 == 0) {
             unsigned char *f2[N];
             void *o[N];
@@ -69,6 +105,16 @@ main(void)
     for (int i = 0; i < N; i++)
         o[i] = frag[i] = malloc(512 * NST);
     ec_method_encode(&list, sizeof(data), data, o);
+    {
+        void *o2[N2];
+        for (size_t i = 0; i < sizeof(data16); i++)
+            data16[i] = (unsigned char)(i * 2246822519u >> 11);
+        if (ec_method_init(NULL, &list16, K2, N2, 2 * N2, "auto") != 0)
+            return 2;
+        for (int i = 0; i < N2; i++)
+            o2[i] = frag16[i] = malloc(512 * NST2);
+        ec_method_encode(&list16, sizeof(data16), data16, o2);
+    }
     for (int t = 0; t < THREADS; t++)
         pthread_create(&th[t], NULL, worker, (void *)(size_t)t);
     for (int t = 0; t < THREADS; t++)
@@ -96,8 +142,11 @@ main(void)
     }
     ec_method_fini(&list);
     ec_method_fini(&list); /* idempotent */
+    ec_method_fini(&list16);
     for (int i = 0; i < N; i++)
         free(frag[i]);
+    for (int i = 0; i < N2; i++)
+        free(frag16[i]);
     printf("sanitize_check failures=%d\n", failures);
     return failures != 0;
 }

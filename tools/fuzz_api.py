@@ -46,6 +46,7 @@ class Arena:
 
     def __init__(self, kind, dev, rng=None):
         self.kind, self.dev, self.keep, self.regs, self.keep_raw = kind, dev, [], [], []
+        self.keep_dev = []
         self.rng = rng or random.Random(0)
         self.subs = []
 
@@ -61,6 +62,13 @@ class Arena:
             t = torch.empty(n + off, dtype=torch.uint8, device=self.dev)[off:]
             if data is not None:
                 t.copy_(torch.from_numpy(data))
+            # held until the call has synchronised (free()): a device call is
+            # asynchronous on the caller's per-thread stream, which torch's
+            # allocator does not track, so a tensor passed as a temporary
+            # would go back to the allocator -- and to another thread's
+            # buffer -- while the library's kernels may still read it (r04af
+            # passed the partial write's user buffer that way)
+            self.keep_dev.append(t)
             return t
         if self.kind == "registered":     # an existing mapping registered (an iobuf arena)
             m = mmap.mmap(-1, (n + 4095) // 4096 * 4096)
@@ -95,6 +103,7 @@ class Arena:
             p.free()
         for p in self.regs:
             g.ec_method.lib.ec_method_host_unregister(p)
+        self.keep_dev.clear()
 
 
 def host(x):

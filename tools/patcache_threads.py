@@ -27,7 +27,8 @@ import torch  # noqa: E402  (torch first: one HIP runtime)
 import glusterfs_amd as g  # noqa: E402
 
 CHUNK = 512
-K, N, NST, GRP, NMASK = 16, 20, 512, 8, 64
+K, N, NST, GRP = 16, 20, 512, 8
+NMASK = int(os.environ.get("PC_MASKS", "64"))   # 1..7: kernel-argument patterns, no table
 
 
 def run(L, nth, secs, dfr, gp, masks):
@@ -63,7 +64,7 @@ def main():
     rng = np.random.default_rng(3)
     masks = sorted(int(x) for x in rng.choice(allm, NMASK, replace=False))
     dfr = [torch.randint(0, 256, (CHUNK * NST,), dtype=torch.uint8, device="cuda") for _ in range(N)]
-    gp = torch.arange(NST // GRP, dtype=torch.uint8, device="cuda") % NMASK
+    gp = torch.arange(NST // GRP, device="cuda").remainder(NMASK).to(torch.uint8)
     torch.cuda.synchronize()
     lib = os.environ.get("EC_MI355X_LIB") or "in-tree"
     with g.ECMatrixList(K, N) as L:
@@ -71,6 +72,7 @@ def main():
         for nth in (1, 8, 1, 8):
             r = run(L, nth, secs, dfr, gp, masks)
             r["lib"] = os.path.basename(lib)
+            r["masks"] = NMASK
             print(json.dumps(r), flush=True)
 
 

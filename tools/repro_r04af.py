@@ -22,7 +22,10 @@ This tool tests that hypothesis directly:
   cross    two threads: X's writev frees its user tensor on return, Y
            takes a block from torch's allocator and a library call on Y's
            own per-thread stream writes it (another fuzz call's output);
-           whether Y got X's block, and whether X's result was then wrong
+           whether Y got X's block, and whether X's result was then wrong;
+           also with Y on a torch side stream (non-blocking, after
+           wait_stream on torch's current stream), as the fuzzer's
+           stream_chain op wrote its outputs
   fuzz     FUZZ-like threads, the writev of r04af's shape, with the user
            tensor freed before the sync (as the fuzzer did) and kept until
            after it (fixed), mismatches counted for each.
@@ -91,7 +94,7 @@ def order_probe(L, secs):
     return dict(calls=calls, wrong=bad, torch_stream=int(torch.cuda.current_stream().cuda_stream))
 
 
-def cross_probe(L, secs, keep):
+def cross_probe(L, secs, keep, side=False):
     """Two threads.  X queues a backlog on its per-thread stream, then the
     r04af writev with the user tensor freed on return (keep=False) or held
     until after its sync (keep=True); Y then takes a block of the same size
@@ -120,11 +123,18 @@ def cross_probe(L, secs, keep):
                 return
             junk = torch.empty(CHUNK * nst_y, dtype=torch.uint8, device="cuda")
             box["reused"] = junk.data_ptr() == box["p"]
-            L.encode_device(0, None, nst_y, ysrc, [junk] + youts)   # Y's per-thread stream
-            g.sync_device(0)
+            if side:      # as the fuzzer's stream_chain: a torch side stream (non-blocking)
+                st = ys
+                st.wait_stream(torch.cuda.current_stream())
+                L.encode_device(0, st.cuda_stream, nst_y, ysrc, [junk] + youts)
+                st.synchronize()
+            else:
+                L.encode_device(0, None, nst_y, ysrc, [junk] + youts)   # Y's per-thread stream
+                g.sync_device(0)
             box["junk"] = junk
             done.set()
 
+    ys = torch.cuda.Stream()
     ty = threading.Thread(target=y_thread)
     ty.start()
     try:
@@ -193,6 +203,10 @@ def main():
         print("cross probe (freed) done", flush=True)
         res["cross_kept_until_sync"] = cross_probe(L, secs, keep=True)
         print("cross probe (kept) done", flush=True)
+        res["cross_side_freed_before_sync"] = cross_probe(L, secs, keep=False, side=True)
+        print("cross probe, side stream (freed) done", flush=True)
+        res["cross_side_kept_until_sync"] = cross_probe(L, secs, keep=True, side=True)
+        print("cross probe, side stream (kept) done", flush=True)
         res["threads_freed_before_sync"] = fuzz_mode(L, secs, keep=False)
         print("freed mode done", flush=True)
         res["threads_kept_until_sync"] = fuzz_mode(L, secs, keep=True)
