@@ -139,8 +139,6 @@ def cross_probe(L, secs, keep, side=False):
     ty.start()
     try:
         while time.time() < t_end:
-            for _ in range(20):
-                L.encode_device(0, None, nst_big, big, bouts)
             user = rng.integers(0, 256, US, dtype=np.uint8)
             oh = rng.integers(0, 256, S, dtype=np.uint8)
             ot = rng.integers(0, 256, S, dtype=np.uint8)
@@ -149,6 +147,12 @@ def cross_probe(L, secs, keep, side=False):
             dh = torch.from_numpy(oh).cuda()
             dt = torch.from_numpy(ot).cuda()
             du = torch.from_numpy(user).cuda()
+            # the backlog AFTER the inputs exist: a copy on torch's (null)
+            # stream waits for every blocking stream, so made later the
+            # inputs would drain it first (r05c/d's probe did, and saw 0)
+            torch.cuda.synchronize()
+            for _ in range(20):
+                L.encode_device(0, None, nst_big, big, bouts)
             L.writev_encode_device(0, None, HEAD, US, du, dh, dt, outs)
             box["p"] = du.data_ptr()
             held = du if keep else None
