@@ -108,6 +108,55 @@ def test_decode_mixed(ec, oracle, k, n, group, nmasks):
         assert np.array_equal(out[s0 * CHUNK * k:s1 * CHUNK * k], want), (g_, hex(m))
 
 
+def _masks(n, k, count, seed):
+    rng = np.random.default_rng(seed)
+    pool = []
+    while len(pool) < count:
+        m = sum(1 << int(b) for b in rng.choice(n, k, replace=False))
+        if m not in pool:
+            pool.append(m)
+    return pool
+
+
+def test_decode_mixed_repeated_sets_across_volumes(ec, oracle):
+    """The per-thread memo of mixed-call pattern sets (ec_method.c
+    pattern_set, r05): the same sets again and again (memo hits), sets
+    larger than the volume's decode-matrix cache, volumes of different k
+    interleaved on one thread (the memo's buffers are shared and grow), and
+    a volume torn down and re-created in the same ec_matrix_list_t (a new
+    serial: no stale hit).  Every group against the oracle."""
+    geos = [(4, 6), (16, 20), (8, 12)]
+    group, ng = 2, 24
+    nst = group * ng
+    frags = {kn: [rnd(CHUNK * nst, 300 + 31 * kn[0] + f) for f in range(kn[1])] for kn in geos}
+    counts = {(4, 6): (3, 9, 15), (16, 20): (3, 12, 45), (8, 12): (3, 12, 45)}  # C(6, 4) = 15
+    sets = {kn: [_masks(kn[1], kn[0], c, seed=c + kn[0]) for c in counts[kn]] for kn in geos}
+    rng = np.random.default_rng(9)
+
+    def check(L, kn, masks):
+        k, n = kn
+        gm = [masks[int(i)] for i in rng.integers(0, len(masks), ng)]
+        out = np.zeros(CHUNK * k * nst, np.uint8)
+        L.decode_mixed(nst, group, gm, frags[kn], out)
+        for g_, m in enumerate(gm):
+            s0, s1 = g_ * group, (g_ + 1) * group
+            rows = oracle.mask_rows(m)
+            want = oracle.decode(k, rows, [frags[kn][r - 1][s0 * CHUNK:s1 * CHUNK] for r in rows])
+            assert np.array_equal(out[s0 * CHUNK * k:s1 * CHUNK * k], want), (kn, g_, hex(m))
+
+    vols = {kn: ec.ECMatrixList(kn[0], kn[1], gen="none") for kn in geos}
+    try:
+        for it in range(30):
+            kn = geos[it % 3]
+            check(vols[kn], kn, sets[kn][(it // 3) % 3])
+            if it == 14:                                     # same struct, new volume
+                vols[kn].fini()
+                vols[kn] = ec.ECMatrixList(kn[0], kn[1], gen="none")
+    finally:
+        for L in vols.values():
+            L.fini()
+
+
 @pytest.mark.parametrize("k,n", [(4, 6), (8, 12), (16, 20)])
 def test_heal(ec, oracle, k, n):
     nst = 20
