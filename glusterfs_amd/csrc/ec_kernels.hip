@@ -260,6 +260,18 @@ int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSr
     if constexpr (SM == 0)
         if (aligned && nt_staging(nstripes * k * ECD_CHUNK))
             return encode_tiles_la<SM, kLdsDmaNT>(s, k, n, nstripes, src, out);
+    /* a byte-misaligned input (a partial write's interior, or a device
+     * buffer at an odd offset): dword-aligned loads shifted through
+     * registers (SM = 3, ec_kernels_impl.h stage_tile_shift) instead of
+     * LDS-DMA at the caller's byte address, whose loads do not coalesce.
+     * One process, 1 GiB partial writes, interior 3 bytes off, LDS-DMA ->
+     * shift staging (profiles/r05/kb3_r05i_rmw.log; aligned encode beside):
+     * 4+2 0.455 -> 0.431 ms (0.429), 8+4 0.513 -> 0.447 (0.419), 16+4 0.440
+     * -> 0.424 (0.403).  (With ds_bpermute for the neighbour's dword instead
+     * of DPP, 16+4 lost: 0.445 -> 0.455, kb3_r05h_rmw.log -- its row-group
+     * encoder is short of LDS cycles.) */
+    if (((uintptr_t)src.in & 3u) != 0)
+        return encode_tiles_la<3, kLdsDmaDefault>(s, k, n, nstripes, src, out);
     return encode_tiles_la<SM, kLdsDmaDefault>(s, k, n, nstripes, src, out);
 }
 

@@ -509,9 +509,80 @@ __device__ __forceinline__ void stage_tile_realign(uint8_t *lds, const EncSrc sr
                 v4u{d[it][0], d[it][1], d[it][2], d[it][3]};
 }
 
+/* SM = 3 (r05): the same tile, staged through registers from dword-aligned
+ * loads.  A 16-byte LDS-DMA load at a byte-misaligned address is not
+ * coalesced: PMC of the 16+4 partial write (interior 777 bytes off) against
+ * the aligned 16+4 encode, same instruction counts, per 1 GiB launch -- L1
+ * (TCP) cache accesses 1.05e8 vs 3.78e7 (the reads alone 5x), UTCL1
+ * requests 8.9e7 vs 3.8e7, TA busy 85 % vs 69 % of its cycles,
+ * profiles/r05/pmc_rmw16/.  Here each lane loads one 16-byte piece of the
+ * tile in memory order from the dword at or below it (dword-aligned: these
+ * coalesce), takes the first dword of the next piece from the next lane
+ * (which loaded it), funnel-shifts by v_alignbyte_b32 and writes the piece
+ * to its plane-major slot.  A lane whose next piece is not the next 16
+ * bytes of the same buffer (the wave's last lane, a stripe's last piece)
+ * loads that dword itself; it holds the last wanted byte, so no load
+ * touches a page the range does not.  Edge stripes (edge buffer) are
+ * aligned and take no shift. */
+template <int K, int T, int NW, int P0 = 0>
+__device__ __forceinline__ void stage_tile_shift(uint8_t *lds, const EncSrc src, uint64_t t0,
+                                                 uint64_t nstripes, u32 wave, u32 lane)
+{
+    constexpr u32 S = K * ECD_CHUNK;
+    constexpr u32 PS = (K - P0) * 32u;                     /* pieces per stripe, inputs >= P0 */
+    constexpr u32 NP = T * PS;                             /* 16-byte pieces */
+    constexpr u32 IT = (NP + NW * 64 - 1) / (NW * 64);
+    const u32 r_in = (u32)(uintptr_t)src.in & 3u;          /* the interior's shift */
+    u32 d[IT][5], dst[IT], sh[IT];
+    bool own[IT];
+#pragma unroll
+    for (u32 it = 0; it < IT; ++it) {
+        const u32 m = it * (NW * 64) + wave * 64 + lane;   /* piece, memory order */
+        const u32 s = m / PS, o = P0 * ECD_CHUNK + m % PS * 16u;
+        const uint64_t st = t0 + s;
+        dst[it] = ~0u;
+        sh[it] = 0;
+        /* the next 16 bytes are not the next lane's (DPP rows are 16 lanes) */
+        own[it] = (lane & 15u) == 15u || o + 16u == S;
+#pragma unroll
+        for (int w = 0; w < 5; ++w)
+            d[it][w] = 0;
+        if (m < NP && st < nstripes) {
+            const u32 p = o / ECD_CHUNK, b = o % ECD_CHUNK / 64u, q = o % 64u / 16u;
+            dst[it] = ((p * 8 + b) * T + s) * 64u + q * 16u;
+            const bool edge = src.edge && (st == 0 || st == nstripes - 1);
+            const uint8_t *a = edge ? src.edge + (st == 0 ? 0u : S) + o : src.in + st * S + o;
+            sh[it] = edge ? 0u : r_in;
+            const u32 *al = reinterpret_cast<const u32 *>(__builtin_assume_aligned(a - sh[it], 4));
+            const v4u v = *reinterpret_cast<const v4u *>(al);
+            d[it][0] = v.x;
+            d[it][1] = v.y;
+            d[it][2] = v.z;
+            d[it][3] = v.w;
+            if (sh[it] && own[it])
+                d[it][4] = al[4];
+        }
+    }
+#pragma unroll
+    for (u32 it = 0; it < IT; ++it) {
+        /* the next lane's first dword: DPP row_shl:1 (lane i reads lane i + 1
+         * of its 16-lane row) */
+        const u32 nx = (u32)__builtin_amdgcn_update_dpp(0, (int)d[it][0], 0x101, 0xF, 0xF, false);
+        if (dst[it] != ~0u) {
+            const u32 t4 = own[it] ? d[it][4] : nx;
+            const v4u v = {__builtin_amdgcn_alignbyte(d[it][1], d[it][0], sh[it]),
+                           __builtin_amdgcn_alignbyte(d[it][2], d[it][1], sh[it]),
+                           __builtin_amdgcn_alignbyte(d[it][3], d[it][2], sh[it]),
+                           __builtin_amdgcn_alignbyte(t4, d[it][3], sh[it])};
+            *reinterpret_cast<v4u *>(lds + dst[it]) = v;
+        }
+    }
+}
+
 /* SM (staging mode): 0 = LDS-DMA from in; 1 = LDS-DMA, stripes 0 and
  * nstripes - 1 from edge (partial-stripe writes); 2 = through registers
- * (stage_tile_realign, r03 A/B: slower than LDS-DMA at every alignment) */
+ * (stage_tile_realign, r03 A/B: slower than LDS-DMA at every alignment);
+ * 3 = dword-aligned loads through registers (stage_tile_shift, r05) */
 template <int K, int T, int NW, int SM, int LA = kLdsDmaDefault>
 __device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src, uint64_t t0,
                                                   uint64_t nstripes, u32 wave, u32 lane)
@@ -519,6 +590,19 @@ __device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src
     constexpr uint64_t S = (uint64_t)K * ECD_CHUNK;
     if constexpr (SM == 2) {
         stage_tile_realign<K, T, NW>(lds, src, t0, nstripes, wave, lane);
+    } else if constexpr (SM == 3) {
+        stage_tile_shift<K, T, NW>(lds, src, t0, nstripes, wave, lane);
+    } else if constexpr (SM >= 4 && SM <= 6) {
+        /* split (kb3 A/B): inputs below KD by LDS-DMA at the caller's
+         * alignment (TA-bound), the rest shifted through registers (LDS
+         * write-bound): the k = 16 encoder is short of LDS cycles */
+        constexpr int KD = SM == 4 ? K / 2 : SM == 5 ? 3 * K / 4 : K / 4;
+        stage_tile<T, NW, LA>(lds, [&](u32 p, uint64_t st) {
+            const uint8_t *b = st == 0 ? src.edge : st == nstripes - 1 ? src.edge + S
+                                                                       : src.in + st * S;
+            return b + p * ECD_CHUNK;
+        }, KD, t0, nstripes, wave, lane);
+        stage_tile_shift<K, T, NW, KD>(lds, src, t0, nstripes, wave, lane);
     } else if constexpr (SM == 1) {
         stage_tile<T, NW, LA>(lds, [&](u32 p, uint64_t st) {
             const uint8_t *b = st == 0 ? src.edge : st == nstripes - 1 ? src.edge + S

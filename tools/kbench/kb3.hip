@@ -10,6 +10,9 @@
  */
 #include "../../glusterfs_amd/csrc/ec_kernels.hip"
 
+/* ec_device.hip's error record, which the launchers call (not linked here) */
+extern "C" int ecd_hip_fail(const char *, int) { return -EIO; }
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -669,17 +672,42 @@ int main(int argc, char **argv)
                      }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
         if constexpr (K == 16) {
             auto kern = ec_encode_tile_rb<16, 20, 4, 2, true, true, 2>;
+            auto kern3 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 3>;
             const size_t lds = encode_tile_rb_lds<20, 4, 2, true>(16);
             v.push_back({"tile encoder, register staging (SM=2)", bytes, [=](hipStream_t st) {
                              hipLaunchKernelGGL(kern, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
                                                 EncSrc{ushift, edge}, f, nst);
                          }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            v.push_back({"tile encoder, dword-aligned shift staging (SM=3)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern3, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            auto kern4 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 4>;
+            auto kern5 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 5>;
+            auto kern6 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 6>;
+            v.push_back({"split: 8 inputs LDS-DMA, 8 shifted (SM=4)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern4, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            v.push_back({"split: 12 inputs LDS-DMA, 4 shifted (SM=5)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern5, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            v.push_back({"split: 4 inputs LDS-DMA, 12 shifted (SM=6)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern6, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
         } else {
             constexpr int NW = N;
             auto kern = ec_encode_tile_t<K, N, 4, NW, true, (K == 4), true, 2>;
+            auto kern3 = ec_encode_tile_t<K, N, 4, NW, true, (K == 4), true, 3>;
             const size_t lds = encode_tile_t_lds<4, NW, true>(K);
             v.push_back({"tile encoder, register staging (SM=2)", bytes, [=](hipStream_t st) {
                              hipLaunchKernelGGL(kern, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            v.push_back({"tile encoder, dword-aligned shift staging (SM=3)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern3, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
                                                 EncSrc{ushift, edge}, f, nst);
                          }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
         }
