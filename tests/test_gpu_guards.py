@@ -36,7 +36,7 @@ def ec():
     return g
 
 
-@pytest.mark.parametrize("off", [1, 4, 8])
+@pytest.mark.parametrize("off", [1, 3, 4, 8, 13])
 @pytest.mark.parametrize("k,n,nst", [(4, 6, 1000), (8, 12, (1 << 17) + 5), (16, 20, 777),
                                      (5, 7, 300)])
 def test_encode_device_misaligned_input(ec, oracle, k, n, nst, off):

@@ -107,6 +107,38 @@ def test_writev_device_matches_oracle(ec, oracle, torch_cuda, k, n):
                 assert np.array_equal(out[i].cpu().numpy(), want[i]), (ci, head, us, mis, i)
 
 
+@pytest.mark.parametrize("k,n", [(4, 6), (8, 12), (16, 20)])
+def test_writev_device_every_byte_shift(ec, oracle, torch_cuda, k, n):
+    """The interior's address modulo 16 takes every value (r05: a byte-
+    misaligned interior is staged from dword-aligned loads, shifted by the
+    byte offset, with the next piece's first dword taken from the
+    neighbouring lane -- 16-lane DPP rows, stripe ends and the wave's last
+    lane load their own), over 11 stripes (several 4-stripe tiles)."""
+    torch = torch_cuda
+    S = CHUNK * k
+    with ec.ECMatrixList(k, n) as L:
+        for shift in range(16):
+            head = 700 + 37 * shift
+            us = 10 * S - head + 333
+            mis = (shift + head) % 16          # (user - head) % 16 == shift
+            base = rnd(us + 32, seed=1000 + shift)
+            user_h = base[mis:mis + us]
+            dbase = torch.from_numpy(base).cuda()
+            duser = dbase[mis:mis + us]
+            assert (duser.data_ptr() - head) % 16 == shift
+            old_head, old_tail = rnd(S, seed=2000 + shift), rnd(S, seed=3000 + shift)
+            dh, dt = torch.from_numpy(old_head).cuda(), torch.from_numpy(old_tail).cuda()
+            want = oracle.encode(k, n, oracle.writev_merge(k, head, user_h, old_head, old_tail))
+            nst = want[0].size // CHUNK
+            out = [torch.full((CHUNK * nst,), 0xA5, dtype=torch.uint8, device="cuda")
+                   for _ in range(n)]
+            torch.cuda.synchronize()
+            L.writev_encode_device(0, None, head, us, duser, dh, dt, out)
+            torch.cuda.synchronize()
+            for i in range(n):
+                assert np.array_equal(out[i].cpu().numpy(), want[i]), (shift, "fragment", i)
+
+
 def test_writev_host_pointer_to_device_dispatch(ec, oracle, torch_cuda):
     """ec_method_writev_encode with device buffers takes the fused path."""
     torch = torch_cuda
