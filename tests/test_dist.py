@@ -118,12 +118,15 @@ def _strong_worker(rank, world, port, nstripes, q):
     q.put((rank, ok, s0, s1))
 
 
-def test_two_rank_strong_job():
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_rank_strong_job(world):
+    """2 ranks, and 4 (a rehearsal of more ranks than the CI's gloo pair;
+    the 8-GPU run is the driver's)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    world, nst = 2, 1001
+    nst = 1001
     ps = [ctx.Process(target=_strong_worker, args=(r, world, port, nst, q)) for r in range(world)]
     for p in ps:
         p.start()
@@ -131,7 +134,8 @@ def test_two_rank_strong_job():
     for p in ps:
         p.join(timeout=60)
     assert all(r[1] for r in res)
-    assert res[0][2] == 0 and res[0][3] == res[1][2] and res[1][3] == nst
+    assert res[0][2] == 0 and res[-1][3] == nst
+    assert all(a[3] == b[2] for a, b in zip(res, res[1:]))     # contiguous, disjoint
 
 
 def test_bind_to_node(tmp_path):
