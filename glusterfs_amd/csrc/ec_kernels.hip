@@ -475,7 +475,6 @@ class PatTableCache {
                 e.tick = ++tick_;
                 ref.slot = i;
                 ref.ptr = e.ptr;
-                ++hits_;
                 return 0;
             }
             if (e.inflight == 0 && (e.dev == dev || !e.ptr) &&
@@ -497,7 +496,6 @@ class PatTableCache {
             e.hash = 0;
             e.words.clear();
             drop_readers(e);                  /* their reads are waited for by s */
-            ++evictions_;
         }
         if (e.dev != dev) {                   /* an empty entry moves device */
             drop_readers(e);
@@ -533,7 +531,6 @@ class PatTableCache {
         e.inflight = 1;
         ref.slot = victim;
         ref.ptr = p;
-        ++uploads_;
         return 0;
     }
 
@@ -552,27 +549,20 @@ class PatTableCache {
                     ev = r.ev;
             if (!ev) {
                 prune_readers(e, s);
-                if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess)
+                rc = hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming),
+                            "hipEventCreate(pattern table reader)");
+                if (rc == 0)
                     e.readers.push_back({s, tok, ev});
                 else
-                    rc = hip_ok(hipGetLastError(), "hipEventCreate(pattern table reader)"), ev = nullptr;
+                    ev = nullptr;
             }
-            if (ev && hipEventRecord(ev, s) != hipSuccess)
-                rc = hip_ok(hipGetLastError(), "hipEventRecord(pattern table reader)");
+            if (ev)
+                rc = hip_ok(hipEventRecord(ev, s), "hipEventRecord(pattern table reader)");
             --e.inflight;
         }
         if (rc)                                /* untracked: drain the stream */
             (void)hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize");
         return rc;
-    }
-
-    void stats(uint64_t *hits, uint64_t *uploads, uint64_t *evictions, uint64_t *folds)
-    {
-        std::lock_guard<std::mutex> g(mu_);
-        *hits = hits_;
-        *uploads = uploads_;
-        *evictions = evictions_;
-        *folds = folds_;
     }
 
   private:
@@ -630,7 +620,6 @@ class PatTableCache {
             hipStreamWaitEvent(s, e.readers.front().ev, 0) == hipSuccess) {
             (void)hipEventDestroy(e.readers.front().ev);
             e.readers.erase(e.readers.begin());
-            ++folds_;
         }
         (void)hipGetLastError();
     }
@@ -639,7 +628,7 @@ class PatTableCache {
     static constexpr size_t kMaxReaders = 16;
     std::mutex mu_;
     Entry e_[kEntries];
-    uint64_t tick_ = 0, hits_ = 0, uploads_ = 0, evictions_ = 0, folds_ = 0;
+    uint64_t tick_ = 0;
 };
 
 /* never destroyed: tables and events would be freed after the runtime */
