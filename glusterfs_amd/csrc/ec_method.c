@@ -329,7 +329,7 @@ env_u64(const char *name, uint64_t dflt)
 
 static struct {
     uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, page_gbps_l, always;
-    uint64_t adapt;
+    uint64_t adapt, hybrid, hybrid_share;
 } __attribute__((aligned(64))) ecm_x;
 static pthread_once_t ecm_xover_once __attribute__((aligned(64))) = PTHREAD_ONCE_INIT;
 
@@ -346,6 +346,10 @@ xover_init(void)
     ecm_x.page_gbps_l = env_u64("EC_GPU_PAGEABLE_GBPS_L", 21);
     ecm_x.always = env_u64("EC_GPU_ALWAYS", 0);
     ecm_x.adapt = env_u64("EC_XOVER_ADAPT", 1);
+    ecm_x.hybrid = env_u64("EC_HYBRID", 1);
+    ecm_x.hybrid_share = env_u64("EC_HYBRID_SHARE", 0); /* tests: a fixed GPU share, 1..999 per mille */
+    if (ecm_x.hybrid_share >= 1000)
+        ecm_x.hybrid_share = 0;
 }
 
 enum { ECM_ENCODE = 0, ECM_DECODE = 1 };
@@ -422,13 +426,16 @@ now_ns(void)
     return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
+/* One sample: `user` bytes coded in `ns` by engine `eng`, into the slot of
+ * calls of `call_user` bytes (a split call's share, r05, is a sample of the
+ * rate its engine reaches inside calls of the whole call's size). */
 static void
-obs_record(int eng, int op, uint32_t k, uint64_t user, uint64_t ns)
+obs_record_part(int eng, int op, uint32_t k, uint64_t call_user, uint64_t user, uint64_t ns)
 {
-    ecm_obs_t *o = obs_slot(eng, op, k, user);
+    ecm_obs_t *o = obs_slot(eng, op, k, call_user);
     uint64_t old, upd, sample;
 
-    if (user < ECM_OBS_MIN || ns == 0 || !ecm_x.adapt)
+    if (call_user < ECM_OBS_MIN || user == 0 || ns == 0 || !ecm_x.adapt)
         return;
     __atomic_store_n(&o->lost, 0, __ATOMIC_RELAXED);
     /* the first call of an engine pays its cold start (page faults on fresh
@@ -441,6 +448,12 @@ obs_record(int eng, int op, uint32_t k, uint64_t user, uint64_t ns)
         upd = old ? old + ((int64_t)sample - (int64_t)old) / 4 : sample;
     while (!__atomic_compare_exchange_n(&o->kbps, &old, upd, 1, __ATOMIC_RELAXED,
                                         __ATOMIC_RELAXED));
+}
+
+static void
+obs_record(int eng, int op, uint32_t k, uint64_t user, uint64_t ns)
+{
+    obs_record_part(eng, op, k, user, user, ns);
 }
 
 static double
@@ -475,38 +488,198 @@ obs_explore(int eng, int op, uint32_t k, uint64_t user)
  * run_decode_dev); `infl`: bytes queued on the least-loaded host GPU.  The
  * model's GPU cost is interpolated between the two pure cases by the staged
  * fraction. */
+/* The two estimates of a host call, in microseconds: `cpu` on the calling
+ * thread, `gpu` on the least-loaded host GPU with `infl` bytes queued ahead
+ * of it, `lat` the GPU's fixed part; returns 1 when `gpu` comes from an
+ * observed rate (which includes the call's latency). */
 static int
-route_cpu_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t staged,
-            uint64_t infl)
+xover_costs(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t staged,
+            uint64_t infl, double *cpu, double *gpu, double *lat)
 {
     static const double isa_f[] = {0.4, 0.7, 1.0};
-    double cpu_gbps, cpu_us, gpu_us, q, obs, f, page_gbps;
+    double cpu_gbps, q, obs, f, page_gbps;
 
-    pthread_once(&ecm_xover_once, xover_init);
-    if (ecm_x.always)
-        return 0;
-    if (moved < ecm_x.cpu_below || infl == UINT64_MAX)
-        return 1;
     cpu_gbps = (op == ECM_ENCODE ? (double)ecm_x.enc_k2 / (k + 2) : (double)ecm_x.dec_k / k) *
                isa_f[isa < 0 ? 0 : isa > 2 ? 2 : isa];
     if ((obs = obs_gbps(ECM_OBS_CPU, op, k, user)) > 0)
         cpu_gbps = obs;
     if (moved >= (32u << 20))
         cpu_gbps = cpu_gbps < 24.0 ? cpu_gbps : 24.0;
-    cpu_us = (double)user / (cpu_gbps * 1e3);
+    *cpu = (double)user / (cpu_gbps * 1e3);
     q = (double)infl * ((double)user / (double)moved); /* queued user bytes */
     if (staged > moved)
         staged = moved;
+    f = (double)staged / (double)moved;
+    *lat = (double)ecm_x.pin_us + f * ((double)ecm_x.page_us - (double)ecm_x.pin_us);
     obs = obs_gbps(gpu_obs_engine(staged, moved), op, k, user);
-    if (obs > 0) {           /* the observed rate includes the call's latency; a */
-        gpu_us = 1.1 * (q + user) / (obs * 1e3); /* near tie stays on the caller's CPU */
-    } else {
-        f = (double)staged / (double)moved;
-        page_gbps = (double)(user >= (8u << 20) ? ecm_x.page_gbps_l : ecm_x.page_gbps);
-        gpu_us = (double)ecm_x.pin_us + f * ((double)ecm_x.page_us - (double)ecm_x.pin_us) +
-                 (q + user) * ((1.0 - f) / (double)ecm_x.pin_gbps + f / page_gbps) / 1e3;
+    if (obs > 0) {
+        *gpu = (q + user) / (obs * 1e3);
+        return 1;
     }
+    page_gbps = (double)(user >= (8u << 20) ? ecm_x.page_gbps_l : ecm_x.page_gbps);
+    *gpu = *lat + (q + user) * ((1.0 - f) / (double)ecm_x.pin_gbps + f / page_gbps) / 1e3;
+    return 0;
+}
+
+static int
+route_cpu_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t staged,
+            uint64_t infl)
+{
+    double cpu_us, gpu_us, lat;
+
+    pthread_once(&ecm_xover_once, xover_init);
+    if (ecm_x.always)
+        return 0;
+    if (moved < ecm_x.cpu_below || infl == UINT64_MAX)
+        return 1;
+    /* a near tie on observed rates stays on the caller's CPU */
+    if (xover_costs(k, isa, user, moved, op, staged, infl, &cpu_us, &gpu_us, &lat))
+        gpu_us *= 1.1;
     return cpu_us <= gpu_us;
+}
+
+/* Split calls (r05).  A host call the two engines would code in comparable
+ * times runs on both: the GPU takes the first f of its stripes (submitted
+ * from a helper thread, as the device layer's host path blocks) while the
+ * calling thread codes the rest on the CPU engine.  With C and G the whole
+ * call's CPU and GPU estimates (the GPU's queue included) and L the GPU's
+ * fixed latency, the share f finishes in max(L + f (G - L), (1 - f) C),
+ * balanced at f = (C - L) / (C + G - L).  Calls below 1 MiB of user data,
+ * or a share under 15 % either way, stay whole (the hand-off costs ~10 us).
+ * Returns f in thousandths, or -1 for no split.  EC_HYBRID=0 turns splits
+ * off; EC_HYBRID_SHARE fixes f (tests). */
+#define ECM_HYBRID_MIN (1u << 20)
+
+static int
+hybrid_share_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t staged,
+               uint64_t infl)
+{
+    double c, g, lat, f;
+
+    pthread_once(&ecm_xover_once, xover_init);
+    if (!ecm_x.hybrid || ecm_x.always || user < ECM_HYBRID_MIN || moved < ecm_x.cpu_below ||
+        infl == UINT64_MAX || staged == ECM_STAGED_UNKNOWN)
+        return -1;
+    if (ecm_x.hybrid_share)
+        return (int)ecm_x.hybrid_share;
+    xover_costs(k, isa, user, moved, op, staged, infl, &c, &g, &lat);
+    if (g <= lat || c <= lat)
+        return -1;
+    f = (c - lat) / (c + g - lat);
+    return f < 0.15 || f > 0.85 ? -1 : (int)(f * 1000.0);
+}
+
+static int
+hybrid_share(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, uint64_t staged)
+{
+    if (ctx->engine == ECM_ENGINE_CPU)
+        return -1;
+    return hybrid_share_q(ctx->k, ctx->isa, user, moved, op, staged, ecd_host_inflight());
+}
+
+/* Helper threads that run the GPU share of split calls (at most 8; a call
+ * finding none free is not split). */
+typedef struct ecm_task {
+    int (*fn)(void *);
+    void *arg;
+    int rc, done;
+    uint64_t ns;                 /* the share's duration */
+    char err[256];               /* its error text when it failed */
+    struct ecm_task *next;
+} ecm_task_t;
+
+#define ECM_HELPERS_MAX 8
+static pthread_mutex_t ecm_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t ecm_pool_cv = PTHREAD_COND_INITIALIZER;
+static pthread_cond_t ecm_done_cv = PTHREAD_COND_INITIALIZER;
+static ecm_task_t *ecm_q_head, **ecm_q_tail = &ecm_q_head;
+static int ecm_helpers, ecm_helpers_idle, ecm_q_len;
+
+static void *
+helper_main(void *unused)
+{
+    ecm_task_t *t;
+    uint64_t seq, t0;
+    int rc;
+
+    (void)unused;
+    pthread_mutex_lock(&ecm_pool_mu);
+    for (;;) {
+        while (!ecm_q_head) {
+            ecm_helpers_idle++;
+            pthread_cond_wait(&ecm_pool_cv, &ecm_pool_mu);
+            ecm_helpers_idle--;
+        }
+        t = ecm_q_head;
+        ecm_q_head = t->next;
+        if (!ecm_q_head)
+            ecm_q_tail = &ecm_q_head;
+        ecm_q_len--;
+        pthread_mutex_unlock(&ecm_pool_mu);
+        seq = ecd_error_seq();
+        t0 = now_ns();
+        rc = t->fn(t->arg);
+        t->ns = now_ns() - t0;
+        t->err[0] = 0;
+        if (rc && ecd_error_seq() != seq)
+            snprintf(t->err, sizeof t->err, "%s", ecd_last_error());
+        pthread_mutex_lock(&ecm_pool_mu);
+        t->rc = rc;
+        t->done = 1;
+        pthread_cond_broadcast(&ecm_done_cv);
+    }
+    return NULL;
+}
+
+/* 0: queued for a free helper; -1: none free (the caller does not split) */
+static int
+helper_submit(ecm_task_t *t)
+{
+    pthread_attr_t at;
+    pthread_t th;
+    int ok = 1;
+
+    t->done = 0;
+    t->next = NULL;
+    pthread_mutex_lock(&ecm_pool_mu);
+    if (ecm_helpers_idle <= ecm_q_len) {
+        ok = ecm_helpers < ECM_HELPERS_MAX && pthread_attr_init(&at) == 0;
+        if (ok) {
+            pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+            ok = pthread_create(&th, &at, helper_main, NULL) == 0;
+            pthread_attr_destroy(&at);
+        }
+        if (ok)
+            ecm_helpers++;
+    }
+    if (ok) {
+        *ecm_q_tail = t;
+        ecm_q_tail = &t->next;
+        ecm_q_len++;
+        pthread_cond_signal(&ecm_pool_cv);
+    }
+    pthread_mutex_unlock(&ecm_pool_mu);
+    return ok ? 0 : -1;
+}
+
+static void
+helper_wait(ecm_task_t *t)
+{
+    pthread_mutex_lock(&ecm_pool_mu);
+    while (!t->done)
+        pthread_cond_wait(&ecm_done_cv, &ecm_pool_mu);
+    pthread_mutex_unlock(&ecm_pool_mu);
+}
+
+/* Stripes of a split call's GPU share: `share` thousandths of nstripes, a
+ * multiple of `unit` (pattern groups), leaving each engine at least one
+ * unit; 0 when the call is too short to split. */
+static uint64_t
+split_stripes(uint64_t nstripes, int share, uint64_t unit)
+{
+    const uint64_t sg = nstripes * (uint64_t)share / 1000u / unit * unit;
+
+    return sg >= unit && sg + unit <= nstripes ? sg : 0;
 }
 
 static int
@@ -556,6 +729,15 @@ ec_method_xover_route(uint32_t k, int32_t op, uint64_t user, uint64_t moved, uin
     if (k < 1 || k > ECM_MAX_K || moved == 0 || (op != ECM_ENCODE && op != ECM_DECODE))
         return -EINVAL;
     return route_cpu_q(k, ecc_isa_max(), user, moved, op, staged, inflight);
+}
+
+int32_t
+ec_method_xover_split(uint32_t k, int32_t op, uint64_t user, uint64_t moved, uint64_t staged,
+                      uint64_t inflight)
+{
+    if (k < 1 || k > ECM_MAX_K || moved == 0 || (op != ECM_ENCODE && op != ECM_DECODE))
+        return -EINVAL;
+    return hybrid_share_q(k, ecc_isa_max(), user, moved, op, staged, inflight);
 }
 
 int32_t
@@ -1147,6 +1329,60 @@ enc_staged(const void *arg)
            staged_bytes((const void *const *)b->out, b->n, b->fl);
 }
 
+/* the GPU share of a split encode (helper thread) */
+struct enc_share {
+    const ecm_ctx_t *ctx;
+    uint64_t nstripes;
+    const void *in;
+    void *const *out;
+};
+
+static int
+enc_share_gpu(void *a)
+{
+    const struct enc_share *e = (const struct enc_share *)a;
+
+    return ecd_encode_host(0, e->ctx->k, e->ctx->n, e->nstripes, e->in, e->out,
+                           e->ctx->enc_pat);
+}
+
+/* A split host encode: stripes [0, sg) on a GPU, the rest on the CPU engine
+ * meanwhile; a failed GPU share is redone on the CPU.  -EAGAIN: not split. */
+static int
+encode_split(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out, int share,
+             uint64_t staged)
+{
+    const uint64_t S = (uint64_t)ctx->k * EC_METHOD_CHUNK_SIZE, user = nstripes * S;
+    const uint64_t sg = split_stripes(nstripes, share, 1);
+    struct enc_share es = {ctx, sg, in, out};
+    ecm_task_t t = {enc_share_gpu, &es, 0, 0, 0, "", NULL};
+    uint8_t *o2[ECM_MAX_N];
+    uint64_t t0;
+    uint32_t i;
+
+    if (!sg || helper_submit(&t) != 0)
+        return -EAGAIN;
+    for (i = 0; i < ctx->n; i++)
+        o2[i] = (uint8_t *)out[i] + sg * EC_METHOD_CHUNK_SIZE;
+    t0 = now_ns();
+    ecc_encode(ctx->isa, ctx->k, ctx->n, nstripes - sg, (const uint8_t *)in + sg * S, o2);
+    obs_record_part(ECM_OBS_CPU, ECM_ENCODE, ctx->k, user, (nstripes - sg) * S, now_ns() - t0);
+    stat_add(ECM_STAT_CPU);
+    helper_wait(&t);
+    if (t.rc == 0) {
+        stat_add(ECM_STAT_GPU);
+        obs_record_part(gpu_obs_engine(staged, nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n)),
+                        ECM_ENCODE, ctx->k, user, sg * S, t.ns);
+        return 0;
+    }
+    if (t.err[0])
+        ecd_set_error(t.err);
+    if (!gpu_failed(t.rc))
+        return t.rc;
+    ecc_encode(ctx->isa, ctx->k, ctx->n, sg, (const uint8_t *)in, (uint8_t *const *)out);
+    return 0;
+}
+
 static int
 host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
 {
@@ -1154,9 +1390,13 @@ host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
     const uint64_t bytes = fl * (ctx->k + ctx->n);
     const struct enc_bufs eb = {in, out, ctx->k, ctx->n, fl};
     uint64_t t0, staged = ECM_STAGED_UNKNOWN;
-    int rc;
+    int rc, gpu, share;
 
-    if (route_gpu(ctx, user, bytes, ECM_ENCODE, enc_staged, &eb, &staged)) {
+    gpu = route_gpu(ctx, user, bytes, ECM_ENCODE, enc_staged, &eb, &staged);
+    share = hybrid_share(ctx, user, bytes, ECM_ENCODE, staged);
+    if (share > 0 && (rc = encode_split(ctx, nstripes, in, out, share, staged)) != -EAGAIN)
+        return rc;
+    if (gpu) {
         t0 = now_ns();
         rc = ecd_encode_host(0, ctx->k, ctx->n, nstripes, in, out, ctx->enc_pat);
         if (!gpu_failed(rc)) {
@@ -1196,6 +1436,95 @@ dec_staged(const void *arg)
                     : (ecd_host_mapped(b->out, b->fl * b->rows) ? 0 : b->fl * b->rows));
 }
 
+/* The arguments of a host combination (ecd_decode_host's). */
+struct dec_call {
+    uint32_t k, rows, nfrags, npat, shift;
+    uint64_t nstripes;
+    const void *const *frags;
+    void *out;
+    void *const *outs;
+    const uint8_t *pats, *gp;
+};
+
+static int
+dec_share_gpu(void *a)
+{
+    const struct dec_call *c = (const struct dec_call *)a;
+
+    return ecd_decode_host(0, c->k, c->rows, c->nstripes, c->nfrags, c->frags, c->out, c->outs,
+                           c->npat, c->pats, c->gp, c->shift);
+}
+
+/* Stripes [s0, s1) of a host combination on the CPU engine (s0: a multiple
+ * of the pattern group). */
+static int
+cpu_decode(const ecm_ctx_t *ctx, const struct dec_call *c, uint64_t s0, uint64_t s1)
+{
+    ecd_combine_desc_t d;
+    uint32_t f, r;
+
+    memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
+    d.k = c->k;
+    d.rows = c->rows;
+    d.nstripes = s1 - s0;
+    d.in_stride = EC_METHOD_CHUNK_SIZE;
+    for (f = 0; f < c->nfrags; f++)      /* NULL: a fragment no pattern reads */
+        d.in_base[f] = c->frags[f] ? (const uint8_t *)c->frags[f] + s0 * EC_METHOD_CHUNK_SIZE
+                                   : NULL;
+    if (c->outs) {
+        d.out_stride = EC_METHOD_CHUNK_SIZE;
+        for (r = 0; r < c->rows; r++)
+            d.out_base[r] = (uint8_t *)c->outs[r] + s0 * EC_METHOD_CHUNK_SIZE;
+    } else {
+        d.out_stride = (uint64_t)c->rows * EC_METHOD_CHUNK_SIZE;
+        for (r = 0; r < c->rows; r++)
+            d.out_base[r] = (uint8_t *)c->out + s0 * d.out_stride + (uint64_t)r * EC_METHOD_CHUNK_SIZE;
+    }
+    d.npatterns = c->npat;
+    d.pat_bytes = c->k + c->rows * c->k;
+    d.pat_ext = c->pats;
+    d.group_pattern = c->gp ? c->gp + (s0 >> c->shift) : NULL;
+    d.group_shift = c->shift;
+    return ecc_combine(ctx->isa, &d);
+}
+
+/* A split host combination: [0, sg) on a GPU, the rest here on the CPU
+ * engine; a failed GPU share is redone on the CPU.  -EAGAIN: not split. */
+static int
+decode_split(ecm_ctx_t *ctx, const struct dec_call *c, int share, uint64_t staged)
+{
+    const uint64_t unit = c->gp ? 1ull << c->shift : 1;
+    const uint64_t sg = split_stripes(c->nstripes, share, unit);
+    const uint64_t per = (uint64_t)c->k * EC_METHOD_CHUNK_SIZE, user = c->nstripes * per;
+    struct dec_call g = *c;
+    ecm_task_t t = {dec_share_gpu, &g, 0, 0, 0, "", NULL};
+    uint64_t t0;
+    int rc;
+
+    g.nstripes = sg;
+    if (!sg || helper_submit(&t) != 0)
+        return -EAGAIN;
+    t0 = now_ns();
+    rc = cpu_decode(ctx, c, sg, c->nstripes);
+    if (rc == 0) {
+        obs_record_part(ECM_OBS_CPU, ECM_DECODE, c->k, user, (c->nstripes - sg) * per,
+                        now_ns() - t0);
+        stat_add(ECM_STAT_CPU);
+    }
+    helper_wait(&t);
+    if (t.rc == 0) {
+        stat_add(ECM_STAT_GPU);
+        obs_record_part(gpu_obs_engine(staged, c->nstripes * EC_METHOD_CHUNK_SIZE * (c->k + c->rows)),
+                        ECM_DECODE, c->k, user, sg * per, t.ns);
+        return rc;
+    }
+    if (t.err[0])
+        ecd_set_error(t.err);
+    if (!gpu_failed(t.rc))
+        return t.rc;
+    return rc ? rc : cpu_decode(ctx, c, 0, sg);
+}
+
 /* Host-buffer combination (decode, mixed decode, heal): the GPU pipeline or
  * the CPU engine, same arguments as ecd_decode_host. */
 static int
@@ -1206,12 +1535,15 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
     const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (k + rows);
     const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE;
     const struct dec_bufs db = {frags, nfrags, out, outs, rows, fl};
-    ecd_combine_desc_t d;
-    uint32_t f, r;
+    const struct dec_call call = {k, rows, nfrags, npat, shift, nstripes, frags, out, outs, pats, gp};
     uint64_t t0, staged = ECM_STAGED_UNKNOWN;
-    int rc;
+    int rc, gpu, share;
 
-    if (route_gpu(ctx, fl * k, bytes, ECM_DECODE, dec_staged, &db, &staged)) {
+    gpu = route_gpu(ctx, fl * k, bytes, ECM_DECODE, dec_staged, &db, &staged);
+    share = hybrid_share(ctx, fl * k, bytes, ECM_DECODE, staged);
+    if (share > 0 && (rc = decode_split(ctx, &call, share, staged)) != -EAGAIN)
+        return rc;
+    if (gpu) {
         t0 = now_ns();
         rc = ecd_decode_host(0, k, rows, nstripes, nfrags, frags, out, outs, npat, pats, gp,
                              shift);
@@ -1226,28 +1558,7 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
         }
     }
     t0 = now_ns();
-    memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
-    d.k = k;
-    d.rows = rows;
-    d.nstripes = nstripes;
-    d.in_stride = EC_METHOD_CHUNK_SIZE;
-    for (f = 0; f < nfrags; f++)
-        d.in_base[f] = frags[f];
-    if (outs) {
-        d.out_stride = EC_METHOD_CHUNK_SIZE;
-        for (r = 0; r < rows; r++)
-            d.out_base[r] = outs[r];
-    } else {
-        d.out_stride = (uint64_t)rows * EC_METHOD_CHUNK_SIZE;
-        for (r = 0; r < rows; r++)
-            d.out_base[r] = (uint8_t *)out + (uint64_t)r * EC_METHOD_CHUNK_SIZE;
-    }
-    d.npatterns = npat;
-    d.pat_bytes = k + rows * k;
-    d.pat_ext = pats;
-    d.group_pattern = gp;
-    d.group_shift = shift;
-    rc = ecc_combine(ctx->isa, &d);
+    rc = cpu_decode(ctx, &call, 0, nstripes);
     if (rc == 0) {
         if (ctx->engine != ECM_ENGINE_CPU)
             obs_record(ECM_OBS_CPU, ECM_DECODE, k, fl * k, now_ns() - t0);
@@ -1351,6 +1662,48 @@ rows_pattern(const ecm_ctx_t *ctx, uintptr_t row_mask, void *const *out, uint8_t
  * same bytes) and not recorded: its rate per user byte is neither an
  * encode's nor a full decode's, and exploration calls that never record
  * would recur forever. */
+/* Stripes [s0, s1) of a row-masked encode on the CPU engine. */
+static int
+cpu_encode_rows(const ecm_ctx_t *ctx, uint64_t s0, uint64_t s1, const void *in, uint32_t m,
+                void *const *outs, const uint8_t *pat)
+{
+    const uint64_t S = (uint64_t)ctx->k * EC_METHOD_CHUNK_SIZE;
+    ecd_combine_desc_t d;
+    uint32_t p;
+
+    memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
+    d.k = ctx->k;
+    d.rows = m;
+    d.nstripes = s1 - s0;
+    d.in_stride = S;
+    d.out_stride = EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < ctx->k; p++)
+        d.in_base[p] = (const uint8_t *)in + s0 * S + (uint64_t)p * EC_METHOD_CHUNK_SIZE;
+    for (p = 0; p < m; p++)
+        d.out_base[p] = (uint8_t *)outs[p] + s0 * EC_METHOD_CHUNK_SIZE;
+    d.npatterns = 1;
+    d.pat_bytes = ctx->k + m * ctx->k;
+    d.pat_ext = pat;
+    return ecc_combine(ctx->isa, &d);
+}
+
+struct rows_share {
+    const ecm_ctx_t *ctx;
+    uint64_t nstripes;
+    const void *in;
+    uint32_t m;
+    void *const *outs;
+    const uint8_t *pat;
+};
+
+static int
+rows_share_gpu(void *a)
+{
+    const struct rows_share *r = (const struct rows_share *)a;
+
+    return ecd_encode_host_rows(0, r->ctx->k, r->m, r->nstripes, r->in, r->outs, r->pat);
+}
+
 static int
 host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
                  void *const *outs, const uint8_t *pat)
@@ -1358,33 +1711,44 @@ host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
     const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE, user = fl * ctx->k;
     const uint64_t bytes = fl * (ctx->k + m);
     const struct enc_bufs eb = {in, outs, ctx->k, m, fl};
-    ecd_combine_desc_t d;
-    uint32_t p;
-    int rc;
+    uint64_t staged = ECM_STAGED_UNKNOWN, sg;
+    int rc, share;
 
-    if (!route_cpu(ctx, user, bytes, ECM_DECODE, 0) &&
-        !route_cpu(ctx, user, bytes, ECM_DECODE, enc_staged(&eb))) {
-        rc = ecd_encode_host_rows(0, ctx->k, m, nstripes, in, outs, pat);
-        if (!gpu_failed(rc)) {
-            if (rc == 0)
-                stat_add(ECM_STAT_GPU);
-            return rc;
+    if (!route_cpu(ctx, user, bytes, ECM_DECODE, 0)) {
+        staged = enc_staged(&eb);
+        /* a near tie: the GPU takes the first share, the CPU the rest */
+        share = hybrid_share(ctx, user, bytes, ECM_DECODE, staged);
+        sg = share > 0 ? split_stripes(nstripes, share, 1) : 0;
+        if (sg) {
+            struct rows_share rs = {ctx, sg, in, m, outs, pat};
+            ecm_task_t t = {rows_share_gpu, &rs, 0, 0, 0, "", NULL};
+
+            if (helper_submit(&t) == 0) {
+                rc = cpu_encode_rows(ctx, sg, nstripes, in, m, outs, pat);
+                if (rc == 0)
+                    stat_add(ECM_STAT_CPU);
+                helper_wait(&t);
+                if (t.rc == 0) {
+                    stat_add(ECM_STAT_GPU);
+                    return rc;
+                }
+                if (t.err[0])
+                    ecd_set_error(t.err);
+                if (!gpu_failed(t.rc))
+                    return t.rc;
+                return rc ? rc : cpu_encode_rows(ctx, 0, sg, in, m, outs, pat);
+            }
+        }
+        if (!route_cpu(ctx, user, bytes, ECM_DECODE, staged)) {
+            rc = ecd_encode_host_rows(0, ctx->k, m, nstripes, in, outs, pat);
+            if (!gpu_failed(rc)) {
+                if (rc == 0)
+                    stat_add(ECM_STAT_GPU);
+                return rc;
+            }
         }
     }
-    memset(&d, 0, offsetof(ecd_combine_desc_t, pat));
-    d.k = ctx->k;
-    d.rows = m;
-    d.nstripes = nstripes;
-    d.in_stride = (uint64_t)ctx->k * EC_METHOD_CHUNK_SIZE;
-    d.out_stride = EC_METHOD_CHUNK_SIZE;
-    for (p = 0; p < ctx->k; p++)
-        d.in_base[p] = (const uint8_t *)in + (uint64_t)p * EC_METHOD_CHUNK_SIZE;
-    for (p = 0; p < m; p++)
-        d.out_base[p] = outs[p];
-    d.npatterns = 1;
-    d.pat_bytes = ctx->k + m * ctx->k;
-    d.pat_ext = pat;
-    rc = ecc_combine(ctx->isa, &d);
+    rc = cpu_encode_rows(ctx, 0, nstripes, in, m, outs, pat);
     if (rc == 0)
         stat_add(ECM_STAT_CPU);
     return rc;

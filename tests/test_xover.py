@@ -84,6 +84,37 @@ assert route(16, DEC, 16 * MiB, 0.5) == 1
 assert route(16, DEC, 16 * MiB, 0.0) == 0
 # the queue ahead on the GPU counts: a full queue sends the call to the CPU
 assert route(8, DEC, 4 * MiB, 0.0, infl=1 << 34) == 1
+
+# split calls (r05): the GPU's share of a call both engines code in
+# comparable time balances L + f (G - L) = (1 - f) C
+def split(k, op, user, staged_frac=0.0, infl=0):
+    moved = user * 2 if op == DEC else user + user * (k + 2 * (k // 2)) // k
+    return L.ec_method_xover_split(k, op, user, moved, int(moved * staged_frac), infl)
+
+assert L.ec_method_xover_split(0, DEC, MiB, 2 * MiB, 0, 0) < 0
+L.ec_method_xover_reset()
+assert split(8, DEC, 512 << 10) == -1                 # below 1 MiB: whole
+for _ in range(3):                                    # equal observed rates, 4 MiB calls
+    observe(CPU, DEC, 8, 4 * MiB, 13.0)
+    observe(GMAP, DEC, 8, 4 * MiB, 13.0)
+f = split(8, DEC, 4 * MiB)
+assert 430 <= f <= 500, f                             # just under half: the GPU's latency
+# the faster engine takes the larger share, and a lopsided pair is not split
+observe(GMAP, DEC, 8, 4 * MiB, 30.0)
+observe(GMAP, DEC, 8, 4 * MiB, 30.0)
+g = split(8, DEC, 4 * MiB)
+assert g > f, (f, g)
+for _ in range(8):
+    observe(GMAP, DEC, 8, 4 * MiB, 300.0)
+assert split(8, DEC, 4 * MiB) == -1                   # GPU share > 85 %: whole on the GPU
+# a queue on the GPU shrinks its share, then ends the split
+L.ec_method_xover_reset()
+for _ in range(3):
+    observe(CPU, DEC, 8, 4 * MiB, 13.0)
+    observe(GMAP, DEC, 8, 4 * MiB, 13.0)
+a, b = split(8, DEC, 4 * MiB, infl=0), split(8, DEC, 4 * MiB, infl=4 * MiB)
+assert a > b > 0, (a, b)
+assert split(8, DEC, 4 * MiB, infl=1 << 30) == -1
 print("OK")
 """
 
