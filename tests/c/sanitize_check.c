@@ -90,6 +90,49 @@ worker(void *arg)
     return NULL;
 }
 
+/* ECD_STUB_GPU=1 (the stub's pretend device codes on the CPU engine): calls
+ * of >= 1 MiB split between the device layer, on the library's helper
+ * threads, and the caller (ec_method.c encode_split / decode_split) -- the
+ * helper pool's hand-off under the sanitizers.  4 threads, each its own
+ * 1.6 MiB 4+2 encode, decode and 16-stripe-group mixed decode. */
+enum { BIG = 800 };
+
+static void *
+split_worker(void *arg)
+{
+    const size_t db = (size_t)512 * K * BIG, fb = (size_t)512 * BIG;
+    unsigned char *d = malloc(db), *out = malloc(db), *f[N];
+    void *o[N], *in[K];
+    uint32_t rows[K] = {3, 4, 5, 6};
+    uintptr_t gm[BIG / 16];
+
+    for (size_t i = 0; i < db; i++)
+        d[i] = (unsigned char)((i + (size_t)arg) * 2654435761u >> 11);
+    for (int i = 0; i < N; i++)
+        o[i] = f[i] = malloc(fb);
+    for (int it = 0; it < 6; it++) {
+        if (ec_method_encode_batch(&list, BIG, d, o) != 0)
+            __atomic_add_fetch(&failures, 1, __ATOMIC_RELAXED);
+        for (int i = 0; i < K; i++)
+            in[i] = f[rows[i] - 1];
+        memset(out, 0, db);
+        if (ec_method_decode_batch(&list, BIG, 0x3C, rows, (const void *const *)in, out) != 0 ||
+            memcmp(out, d, db) != 0)
+            __atomic_add_fetch(&failures, 1, __ATOMIC_RELAXED);
+        for (size_t g = 0; g < BIG / 16; g++)
+            gm[g] = g & 1 ? 0x3C : 0x0F;
+        memset(out, 0, db);
+        if (ec_method_decode_mixed(&list, BIG, 16, gm, (const void *const *)f, out) != 0 ||
+            memcmp(out, d, db) != 0)
+            __atomic_add_fetch(&failures, 1, __ATOMIC_RELAXED);
+    }
+    for (int i = 0; i < N; i++)
+        free(f[i]);
+    free(d);
+    free(out);
+    return NULL;
+}
+
 int
 main(void)
 {
@@ -119,6 +162,21 @@ main(void)
         pthread_create(&th[t], NULL, worker, (void *)(size_t)t);
     for (int t = 0; t < THREADS; t++)
         pthread_join(th[t], NULL);
+    if (getenv("ECD_STUB_GPU")) {
+        ec_method_stats_t st0, st1;
+        ec_method_get_stats(&st0);
+        for (int t = 0; t < 4; t++)
+            pthread_create(&th[t], NULL, split_worker, (void *)(size_t)t);
+        for (int t = 0; t < 4; t++)
+            pthread_join(th[t], NULL);
+        ec_method_get_stats(&st1);
+        /* every call split: both engines counted once per call */
+        if (st1.gpu_calls - st0.gpu_calls < 4 * 6 * 3 || st1.cpu_calls - st0.cpu_calls < 4 * 6 * 3)
+            failures++;
+        printf("split calls: gpu %llu cpu %llu\n",
+               (unsigned long long)(st1.gpu_calls - st0.gpu_calls),
+               (unsigned long long)(st1.cpu_calls - st0.cpu_calls));
+    }
     if (list.count > 3)
         failures++;
     /* trusted.ec.config round trip and checks (ec-helpers.c:298-380) */

@@ -137,19 +137,38 @@ print("XOVER " + json.dumps(res))
 '''
 
 
-def test_crossover_defaults():
-    """Default cost model (no test overrides): FUSE-sized and
-    cache-sized encodes on the calling thread, a 16 MiB 16+4 decode (pageable)
-    and a 64 MiB encode from pinned buffers on the GPU."""
+def _crossover_child(hybrid):
     env = {k: v for k, v in os.environ.items()
-           if not (k.startswith("EC_GPU_") or k.startswith("EC_CPU_"))}
+           if not (k.startswith("EC_GPU_") or k.startswith("EC_CPU_") or k.startswith("EC_HYBRID"))}
     env["EC_MI355X_QUIET"] = "1"
+    env["EC_HYBRID"] = "1" if hybrid else "0"
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.dirname(HERE)], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("XOVER ")][0]
-    res = json.loads(line[6:])
+    return json.loads(line[6:])
+
+
+def test_crossover_defaults():
+    """Default cost model with split calls off (no other overrides, DESIGN.md
+    1.1): FUSE-sized and cache-sized encodes on the calling thread, a 16 MiB
+    16+4 decode (pageable) and a 64 MiB encode from pinned buffers on the GPU."""
+    res = _crossover_child(hybrid=False)
     assert res["enc4+2_128K"] == dict(gpu=0, cpu=1, ok=True), res
     assert res["enc4+2_8M"] == dict(gpu=0, cpu=1, ok=True), res
     assert res["dec16+4_16M"] == dict(gpu=1, cpu=0, ok=True), res
     assert res["enc4+2_64M_pinned"] == dict(gpu=1, cpu=0, ok=True), res
+
+
+def test_crossover_defaults_with_split_calls():
+    """The same calls with split calls on (the default since r05): below
+    1 MiB a call stays whole on its engine; the larger ones run whole on the
+    engine the crossover picks or split across both (gpu and cpu each
+    counted once), and every output is exact."""
+    res = _crossover_child(hybrid=True)
+    assert res["enc4+2_128K"] == dict(gpu=0, cpu=1, ok=True), res
+    for name, whole in (("enc4+2_8M", dict(gpu=0, cpu=1)), ("dec16+4_16M", dict(gpu=1, cpu=0)),
+                        ("enc4+2_64M_pinned", dict(gpu=1, cpu=0))):
+        got = dict(res[name])
+        assert got.pop("ok") is True, (name, res)
+        assert got in (whole, dict(gpu=1, cpu=1)), (name, res)
