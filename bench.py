@@ -943,6 +943,11 @@ def main():
     if args.gpus is not None and int(world_env or 1) != args.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s: the ranks must match the GPUs"
                  % (args.gpus, world_env))
+    # host-buffer calls made in this process (the PCIe-inclusive e2e lines)
+    # measure the GPU path: without this the crossover could code them on
+    # the CPU engine, or split them across both engines (r05); the heal sweep
+    # and the concurrency probe set the engine per child process themselves
+    os.environ.setdefault("EC_GPU_ALWAYS", "1")
     import torch
     import glusterfs_amd as g
     from glusterfs_amd.dist import Group, local_device_index

@@ -546,8 +546,9 @@ route_cpu_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t
  * fixed latency, the share f finishes in max(L + f (G - L), (1 - f) C),
  * balanced at f = (C - L) / (C + G - L).  Calls below 1 MiB of user data,
  * or a share under 15 % either way, stay whole (the hand-off costs ~10 us).
+ * Only calls whose buffers are all pinned and mapped are split (below).
  * Returns f in thousandths, or -1 for no split.  EC_HYBRID=0 turns splits
- * off; EC_HYBRID_SHARE fixes f (tests). */
+ * off; EC_HYBRID_SHARE fixes f for any call (tests). */
 #define ECM_HYBRID_MIN (1u << 20)
 
 static int
@@ -562,6 +563,13 @@ hybrid_share_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint6
         return -1;
     if (ecm_x.hybrid_share)
         return (int)ecm_x.hybrid_share;
+    /* only zero-copy calls: a staged GPU share is copied by the library's
+     * CPU threads, so beside the CPU share it competes for the same cores --
+     * 8 client threads of 4 MiB 8+4 heal windows on pageable buffers fell
+     * from 41.2 to 26.6 GB/s split (tools/kbench/concur,
+     * profiles/r05/r05o_concur_hybrid.log) */
+    if (staged != 0)
+        return -1;
     xover_costs(k, isa, user, moved, op, staged, infl, &c, &g, &lat);
     if (g <= lat || c <= lat)
         return -1;
