@@ -585,6 +585,20 @@ hybrid_share(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, uint64
     return hybrid_share_q(ctx->k, ctx->isa, user, moved, op, staged, ecd_host_inflight());
 }
 
+/* The split share of a call, querying where its buffers live only when an
+ * all-mapped call of its size would be split (the queries serialise in the
+ * HIP runtime); *staged is filled in when it was queried. */
+static int
+split_share(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op,
+            uint64_t (*staged_of)(const void *), const void *arg, uint64_t *staged)
+{
+    if (hybrid_share(ctx, user, moved, op, 0) <= 0)
+        return -1;
+    if (*staged == ECM_STAGED_UNKNOWN)
+        *staged = staged_of(arg);
+    return hybrid_share(ctx, user, moved, op, *staged);
+}
+
 /* Helper threads that run the GPU share of split calls (at most 8; a call
  * finding none free is not split). */
 typedef struct ecm_task {
@@ -1401,7 +1415,7 @@ host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
     int rc, gpu, share;
 
     gpu = route_gpu(ctx, user, bytes, ECM_ENCODE, enc_staged, &eb, &staged);
-    share = hybrid_share(ctx, user, bytes, ECM_ENCODE, staged);
+    share = split_share(ctx, user, bytes, ECM_ENCODE, enc_staged, &eb, &staged);
     if (share > 0 && (rc = encode_split(ctx, nstripes, in, out, share, staged)) != -EAGAIN)
         return rc;
     if (gpu) {
@@ -1548,7 +1562,7 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
     int rc, gpu, share;
 
     gpu = route_gpu(ctx, fl * k, bytes, ECM_DECODE, dec_staged, &db, &staged);
-    share = hybrid_share(ctx, fl * k, bytes, ECM_DECODE, staged);
+    share = split_share(ctx, fl * k, bytes, ECM_DECODE, dec_staged, &db, &staged);
     if (share > 0 && (rc = decode_split(ctx, &call, share, staged)) != -EAGAIN)
         return rc;
     if (gpu) {
@@ -1722,31 +1736,32 @@ host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
     uint64_t staged = ECM_STAGED_UNKNOWN, sg;
     int rc, share;
 
-    if (!route_cpu(ctx, user, bytes, ECM_DECODE, 0)) {
-        staged = enc_staged(&eb);
-        /* a near tie: the GPU takes the first share, the CPU the rest */
-        share = hybrid_share(ctx, user, bytes, ECM_DECODE, staged);
-        sg = share > 0 ? split_stripes(nstripes, share, 1) : 0;
-        if (sg) {
-            struct rows_share rs = {ctx, sg, in, m, outs, pat};
-            ecm_task_t t = {rows_share_gpu, &rs, 0, 0, 0, "", NULL};
+    /* a near tie: the GPU takes the first share, the CPU the rest */
+    share = split_share(ctx, user, bytes, ECM_DECODE, enc_staged, &eb, &staged);
+    sg = share > 0 ? split_stripes(nstripes, share, 1) : 0;
+    if (sg) {
+        struct rows_share rs = {ctx, sg, in, m, outs, pat};
+        ecm_task_t t = {rows_share_gpu, &rs, 0, 0, 0, "", NULL};
 
-            if (helper_submit(&t) == 0) {
-                rc = cpu_encode_rows(ctx, sg, nstripes, in, m, outs, pat);
-                if (rc == 0)
-                    stat_add(ECM_STAT_CPU);
-                helper_wait(&t);
-                if (t.rc == 0) {
-                    stat_add(ECM_STAT_GPU);
-                    return rc;
-                }
-                if (t.err[0])
-                    ecd_set_error(t.err);
-                if (!gpu_failed(t.rc))
-                    return t.rc;
-                return rc ? rc : cpu_encode_rows(ctx, 0, sg, in, m, outs, pat);
+        if (helper_submit(&t) == 0) {
+            rc = cpu_encode_rows(ctx, sg, nstripes, in, m, outs, pat);
+            if (rc == 0)
+                stat_add(ECM_STAT_CPU);
+            helper_wait(&t);
+            if (t.rc == 0) {
+                stat_add(ECM_STAT_GPU);
+                return rc;
             }
+            if (t.err[0])
+                ecd_set_error(t.err);
+            if (!gpu_failed(t.rc))
+                return t.rc;
+            return rc ? rc : cpu_encode_rows(ctx, 0, sg, in, m, outs, pat);
         }
+    }
+    if (!route_cpu(ctx, user, bytes, ECM_DECODE, 0)) {
+        if (staged == ECM_STAGED_UNKNOWN)
+            staged = enc_staged(&eb);
         if (!route_cpu(ctx, user, bytes, ECM_DECODE, staged)) {
             rc = ecd_encode_host_rows(0, ctx->k, m, nstripes, in, outs, pat);
             if (!gpu_failed(rc)) {
