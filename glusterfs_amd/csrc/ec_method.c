@@ -546,14 +546,30 @@ route_cpu_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t
  * fixed latency, the share f finishes in max(L + f (G - L), (1 - f) C),
  * balanced at f = (C - L) / (C + G - L).  Calls below 1 MiB of user data,
  * or a share under 15 % either way, stay whole (the hand-off costs ~10 us).
- * Only calls whose buffers are all pinned and mapped are split (below).
+ * Calls that stage a buffer split only when no other large call is in
+ * flight (below).
  * Returns f in thousandths, or -1 for no split.  EC_HYBRID=0 turns splits
  * off; EC_HYBRID_SHARE fixes f for any call (tests). */
 #define ECM_HYBRID_MIN (1u << 20)
 
+/* Host calls of >= 1 MiB in flight in the process (own cache line: every
+ * such call writes it twice). */
+static struct {
+    uint32_t n;
+} __attribute__((aligned(64))) ecm_big_calls;
+
+static void
+big_call(uint64_t user, int d)
+{
+    if (user >= ECM_HYBRID_MIN)
+        __atomic_add_fetch(&ecm_big_calls.n, (uint32_t)d, __ATOMIC_RELAXED);
+}
+
+/* `alone`: no other large host call is in flight, so a staged GPU share's
+ * copies do not compete with other callers' CPU work */
 static int
 hybrid_share_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t staged,
-               uint64_t infl)
+               uint64_t infl, int alone)
 {
     double c, g, lat, f;
 
@@ -563,12 +579,13 @@ hybrid_share_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint6
         return -1;
     if (ecm_x.hybrid_share)
         return (int)ecm_x.hybrid_share;
-    /* only zero-copy calls: a staged GPU share is copied by the library's
-     * CPU threads, so beside the CPU share it competes for the same cores --
-     * 8 client threads of 4 MiB 8+4 heal windows on pageable buffers fell
-     * from 41.2 to 26.6 GB/s split (tools/kbench/concur,
-     * profiles/r05/r05o_concur_hybrid.log) */
-    if (staged != 0)
+    /* a staged GPU share is copied by the library's CPU threads, so beside
+     * the CPU share it competes for the same cores: 8 client threads of
+     * 4 MiB 8+4 heal windows on pageable buffers fell from 41.2 to 26.6 GB/s
+     * split (tools/kbench/concur, profiles/r05/r05o_concur_hybrid.log).  So
+     * calls that stage split only while no other large call is in flight
+     * (one stream: 6.5 -> 10.1 GB/s on pageable windows, r05o) */
+    if (staged != 0 && !alone)
         return -1;
     xover_costs(k, isa, user, moved, op, staged, infl, &c, &g, &lat);
     if (g <= lat || c <= lat)
@@ -582,7 +599,8 @@ hybrid_share(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, uint64
 {
     if (ctx->engine == ECM_ENGINE_CPU)
         return -1;
-    return hybrid_share_q(ctx->k, ctx->isa, user, moved, op, staged, ecd_host_inflight());
+    return hybrid_share_q(ctx->k, ctx->isa, user, moved, op, staged, ecd_host_inflight(),
+                          __atomic_load_n(&ecm_big_calls.n, __ATOMIC_RELAXED) <= 1);
 }
 
 /* The split share of a call, querying where its buffers live only when an
@@ -759,7 +777,7 @@ ec_method_xover_split(uint32_t k, int32_t op, uint64_t user, uint64_t moved, uin
 {
     if (k < 1 || k > ECM_MAX_K || moved == 0 || (op != ECM_ENCODE && op != ECM_DECODE))
         return -EINVAL;
-    return hybrid_share_q(k, ecc_isa_max(), user, moved, op, staged, inflight);
+    return hybrid_share_q(k, ecc_isa_max(), user, moved, op, staged, inflight, 0);
 }
 
 int32_t
@@ -1406,7 +1424,7 @@ encode_split(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out
 }
 
 static int
-host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
+host_encode_1(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
 {
     const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE, user = fl * ctx->k;
     const uint64_t bytes = fl * (ctx->k + ctx->n);
@@ -1437,6 +1455,19 @@ host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
         obs_record(ECM_OBS_CPU, ECM_ENCODE, ctx->k, user, now_ns() - t0);
     stat_add(ECM_STAT_CPU);
     return 0;
+}
+
+/* (large calls counted in flight: the split rule for staged calls) */
+static int
+host_encode(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out)
+{
+    const uint64_t user = nstripes * EC_METHOD_CHUNK_SIZE * ctx->k;
+    int rc;
+
+    big_call(user, 1);
+    rc = host_encode_1(ctx, nstripes, in, out);
+    big_call(user, -1);
+    return rc;
 }
 
 struct dec_bufs {
@@ -1550,9 +1581,9 @@ decode_split(ecm_ctx_t *ctx, const struct dec_call *c, int share, uint64_t stage
 /* Host-buffer combination (decode, mixed decode, heal): the GPU pipeline or
  * the CPU engine, same arguments as ecd_decode_host. */
 static int
-host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32_t nfrags,
-            const void *const *frags, void *out, void *const *outs, uint32_t npat,
-            const uint8_t *pats, const uint8_t *gp, uint32_t shift)
+host_decode_1(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32_t nfrags,
+              const void *const *frags, void *out, void *const *outs, uint32_t npat,
+              const uint8_t *pats, const uint8_t *gp, uint32_t shift)
 {
     const uint64_t bytes = nstripes * EC_METHOD_CHUNK_SIZE * (k + rows);
     const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE;
@@ -1586,6 +1617,20 @@ host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32
             obs_record(ECM_OBS_CPU, ECM_DECODE, k, fl * k, now_ns() - t0);
         stat_add(ECM_STAT_CPU);
     }
+    return rc;
+}
+
+static int
+host_decode(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint32_t nfrags,
+            const void *const *frags, void *out, void *const *outs, uint32_t npat,
+            const uint8_t *pats, const uint8_t *gp, uint32_t shift)
+{
+    const uint64_t user = nstripes * EC_METHOD_CHUNK_SIZE * k;
+    int rc;
+
+    big_call(user, 1);
+    rc = host_decode_1(ctx, k, rows, nstripes, nfrags, frags, out, outs, npat, pats, gp, shift);
+    big_call(user, -1);
     return rc;
 }
 
@@ -1727,8 +1772,8 @@ rows_share_gpu(void *a)
 }
 
 static int
-host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
-                 void *const *outs, const uint8_t *pat)
+host_encode_rows_1(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
+                   void *const *outs, const uint8_t *pat)
 {
     const uint64_t fl = nstripes * EC_METHOD_CHUNK_SIZE, user = fl * ctx->k;
     const uint64_t bytes = fl * (ctx->k + m);
@@ -1774,6 +1819,19 @@ host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
     rc = cpu_encode_rows(ctx, 0, nstripes, in, m, outs, pat);
     if (rc == 0)
         stat_add(ECM_STAT_CPU);
+    return rc;
+}
+
+static int
+host_encode_rows(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m,
+                 void *const *outs, const uint8_t *pat)
+{
+    const uint64_t user = nstripes * EC_METHOD_CHUNK_SIZE * ctx->k;
+    int rc;
+
+    big_call(user, 1);
+    rc = host_encode_rows_1(ctx, nstripes, in, m, outs, pat);
+    big_call(user, -1);
     return rc;
 }
 
