@@ -346,9 +346,11 @@ int32_t ec_method_xover_route(uint32_t k, int32_t op, uint64_t user, uint64_t mo
                               uint64_t staged, uint64_t inflight);
 /* Split calls (r05): the share of such a call's stripes, in thousandths, that
  * a GPU codes while the calling thread codes the rest on the CPU engine, or
- * -1 when the call stays whole (below 1 MiB of user data, a buffer that is
- * not pinned and mapped, or one engine would take under 15 %).  Same
- * arguments as ec_method_xover_route. */
+ * -1 when the call stays whole (below 1 MiB of user data, one engine would
+ * take under 15 %, or -- costed as if other large calls were in flight -- a
+ * buffer that is not pinned and mapped: a real call with staged buffers
+ * splits only while it is the only large host call).  Same arguments as
+ * ec_method_xover_route. */
 int32_t ec_method_xover_split(uint32_t k, int32_t op, uint64_t user, uint64_t moved,
                               uint64_t staged, uint64_t inflight);
 int32_t ec_method_xover_observe(int32_t engine, int32_t op, uint32_t k, uint64_t user,

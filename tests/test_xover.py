@@ -115,8 +115,9 @@ for _ in range(3):
 a, b = split(8, DEC, 4 * MiB, infl=0), split(8, DEC, 4 * MiB, infl=4 * MiB)
 assert a > b > 0, (a, b)
 assert split(8, DEC, 4 * MiB, infl=1 << 30) == -1
-# a staged buffer keeps the call whole (its GPU share would be copied by the
-# CPU threads the CPU share needs)
+# a staged buffer keeps the call whole while other large calls are in flight
+# (its GPU share would be copied by the CPU threads the other callers need);
+# the probe costs a call that is not alone
 assert split(8, DEC, 4 * MiB, staged_frac=0.25) == -1
 print("OK")
 """
