@@ -43,6 +43,9 @@
 #include "ec_device.h"
 #include "ec_kernels.h"
 
+static uint64_t hostpage_ttl_ns();   /* the host-page caches' lifetime (below) */
+static uint64_t coarse_ns();
+
 namespace {
 
 constexpr int kMaxDev = 16;
@@ -103,8 +106,14 @@ void set_err_text(std::string s)
     ++t_err_seq;
 }
 
+/* Records a failed HIP call's error as this thread's and consumes the HIP
+ * runtime's sticky copy of it: a failure the library reports by its return
+ * code must not surface again at the caller's next HIP or torch call
+ * (test_register_errors' refused unregister, left pending, failed the next
+ * test's torch copy with hipErrorHostMemoryNotRegistered). */
 void set_err(const char *what, hipError_t e)
 {
+    (void)hipGetLastError();
     set_err_text(std::string(what) + ": " + hipGetErrorString(e) + " (" +
                  std::to_string((int)e) + ")");
 }
@@ -166,6 +175,10 @@ std::atomic<uint64_t> g_ptr_queries{0}, g_map_queries{0};
 /* Generation of the library's own host-memory frees: invalidates the
  * per-thread host-page cache of ecd_ptr_device (below). */
 std::atomic<uint32_t> g_host_gen{0};
+/* Generation of the library's host-memory registrations (every successful
+ * hipHostRegister and pinned allocation): invalidates the per-thread cache of
+ * ranges found unmapped (mapped(), below). */
+std::atomic<uint32_t> g_map_gen{0};
 
 void print_query_counts()
 {
@@ -178,12 +191,16 @@ void discover()
     if (getenv("EC_MI355X_DEBUG") && atoi(getenv("EC_MI355X_DEBUG")))
         atexit(print_query_counts);
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess)
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
         n = 0;
+    }
     for (int i = 0; i < n && g_ndev < kMaxDev; ++i) {
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, i) != hipSuccess)
+        if (hipGetDeviceProperties(&prop, i) != hipSuccess) {
+            (void)hipGetLastError();
             continue;
+        }
         if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
             continue; /* kernels are built for gfx950 only */
         g_dev_ids[g_ndev++] = i;
@@ -411,23 +428,49 @@ void add_gather(std::vector<CopyPool::Piece> &v, uint8_t *dst, const std::vector
  * accesses. */
 bool pool_owns(const void *p, size_t n);
 
+/* Ranges found NOT mapped, per thread (direct-mapped on the start page).
+ * The two hipHostGetDevicePointer queries of a range serialise in the HIP
+ * runtime like the attribute queries (ecd_ptr_device, below): a pageable
+ * 8+4 heal window asks for 22 ranges, and 8 client threads asking on every
+ * call ran 8 % below the CPU engine alone with almost every call on the CPU
+ * (profiles/r05/r05u_busyab.log).  Only the negative verdict is cached, for
+ * EC_HOSTPAGE_MS and until the library registers or pins more memory
+ * (g_map_gen): a stale one stages a buffer that has become mapped -- the
+ * same bytes, coded a little slower -- while a stale positive one would let a
+ * kernel read memory that is no longer mapped, so those are never cached. */
+struct Unmapped {
+    uintptr_t p;
+    size_t n;
+    uint64_t until_ns;
+    uint32_t gen;
+};
+thread_local Unmapped t_unmapped[256];
+
 uint8_t *mapped(const void *p, size_t n)
 {
     if (!p || ((uintptr_t)p & 15))
         return nullptr;
     if (pool_owns(p, n))   /* a pool buffer: registered at the same address */
         return static_cast<uint8_t *>(const_cast<void *>(p));
+    const uint64_t ttl = hostpage_ttl_ns();
+    const uintptr_t pg = (uintptr_t)p >> 12;
+    Unmapped &u = t_unmapped[(uint64_t)(pg * 0x9E3779B97F4A7C15ull) >> 56];
+    const uint32_t gen = g_map_gen.load(std::memory_order_acquire);
+    const uint64_t now = ttl ? coarse_ns() : 0;
+    if (ttl && u.p == (uintptr_t)p && u.n == n && u.gen == gen && now < u.until_ns)
+        return nullptr;
     void *d0 = nullptr, *d1 = nullptr;
     g_map_queries.fetch_add(1, std::memory_order_relaxed);
     if (hipHostGetDevicePointer(&d0, const_cast<void *>(p), 0) != hipSuccess ||
-        (n > 1 && hipHostGetDevicePointer(&d1, (uint8_t *)p + n - 1, 0) != hipSuccess)) {
+        (n > 1 && hipHostGetDevicePointer(&d1, (uint8_t *)p + n - 1, 0) != hipSuccess) ||
+        /* one contiguous mapping, at the same address on both sides (ROCm
+         * maps pinned host memory at its host virtual address) */
+        d0 != p || (n > 1 && (uint8_t *)d1 != (uint8_t *)d0 + n - 1)) {
         (void)hipGetLastError();
+        if (ttl)
+            u = Unmapped{(uintptr_t)p, n, now + ttl, gen};
         return nullptr;
     }
-    /* one contiguous mapping, at the same address on both sides (ROCm maps
-     * pinned host memory at its host virtual address) */
-    if (d0 != p || (n > 1 && (uint8_t *)d1 != (uint8_t *)d0 + n - 1))
-        return nullptr;
     return static_cast<uint8_t *>(d0);
 }
 
@@ -502,6 +545,7 @@ void *pinned_alloc(size_t bytes, int node)
             (void)syscall(SYS_mbind, p, len, 1, mask, (unsigned long)1024, 0u);
             memset(p, 0, len);                       /* fault in on the node */
             if (hipHostRegister(p, len, hipHostRegisterMapped) == hipSuccess) {
+                g_map_gen.fetch_add(1, std::memory_order_release);
                 std::lock_guard<std::mutex> g(g_numa_mu);
                 g_numa_allocs[p] = len;
                 return p;
@@ -515,6 +559,7 @@ void *pinned_alloc(size_t bytes, int node)
         (void)hipGetLastError();
         return nullptr;
     }
+    g_map_gen.fetch_add(1, std::memory_order_release);
     return p;
 }
 
@@ -931,6 +976,7 @@ class RegQueue {
                                     "buffers there stay pageable\n",
                             r.first, r.second, hipGetErrorString(e));
             } else {
+                g_map_gen.fetch_add(1, std::memory_order_release);
                 regs_.fetch_add(1, std::memory_order_relaxed);
                 reg_us_.fetch_add(dt, std::memory_order_relaxed);
             }
@@ -1774,6 +1820,7 @@ int ecd_host_register(void *p, size_t bytes)
         set_err("hipHostRegister", e);
         return e == hipErrorHostMemoryAlreadyRegistered ? -EEXIST : -ENOMEM;
     }
+    g_map_gen.fetch_add(1, std::memory_order_release);
     return 0;
 }
 

@@ -329,7 +329,7 @@ env_u64(const char *name, uint64_t dflt)
 
 static struct {
     uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, page_gbps_l, always;
-    uint64_t adapt, hybrid, hybrid_share;
+    uint64_t adapt, hybrid, hybrid_share, copy_gbps;
 } __attribute__((aligned(64))) ecm_x;
 static pthread_once_t ecm_xover_once __attribute__((aligned(64))) = PTHREAD_ONCE_INIT;
 
@@ -350,6 +350,9 @@ xover_init(void)
     ecm_x.hybrid_share = env_u64("EC_HYBRID_SHARE", 0); /* tests: a fixed GPU share, 1..999 per mille */
     if (ecm_x.hybrid_share >= 1000)
         ecm_x.hybrid_share = 0;
+    /* one CPU thread's copy rate between pageable and pinned memory (the
+     * staging copies of a GPU call with pageable buffers); 0: no busy rule */
+    ecm_x.copy_gbps = env_u64("EC_STAGE_COPY_GBPS", 10);
 }
 
 enum { ECM_ENCODE = 0, ECM_DECODE = 1 };
@@ -521,9 +524,20 @@ xover_costs(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t
     return 0;
 }
 
+/* 0: the GPU; 1: the CPU engine; ECM_ROUTE_CPU_BUSY: the CPU engine because
+ * the call stages buffers while `others` large host calls are in flight (no
+ * exploration of the GPU for it).  The staging copies of a GPU call run on
+ * the library's CPU threads; while other callers keep the cores busy, a call
+ * whose copies take at least as much CPU time as coding it on the calling
+ * thread would (8+4 heal windows on pageable buffers: copying 2-2.5x the user
+ * bytes against a ~7-13 GB/s coder) frees no CPU for them and only adds the
+ * trip to the GPU: 8 threads of 4 MiB heal windows on pageable buffers ran
+ * 40.6 GB/s auto against 47.7 CPU-only (profiles/r05/r05t_concur.log). */
+#define ECM_ROUTE_CPU_BUSY 2
+
 static int
 route_cpu_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t staged,
-            uint64_t infl)
+            uint64_t infl, uint32_t others)
 {
     double cpu_us, gpu_us, lat;
 
@@ -535,6 +549,9 @@ route_cpu_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t
     /* a near tie on observed rates stays on the caller's CPU */
     if (xover_costs(k, isa, user, moved, op, staged, infl, &cpu_us, &gpu_us, &lat))
         gpu_us *= 1.1;
+    if (others && staged && ecm_x.copy_gbps &&
+        (double)(staged < moved ? staged : moved) / ((double)ecm_x.copy_gbps * 1e3) >= cpu_us)
+        return ECM_ROUTE_CPU_BUSY;
     return cpu_us <= gpu_us;
 }
 
@@ -722,12 +739,24 @@ split_stripes(uint64_t nstripes, int share, uint64_t unit)
     return sg >= unit && sg + unit <= nstripes ? sg : 0;
 }
 
+/* other large host calls in flight beside the caller's own (which counts
+ * itself when it is one) */
+static uint32_t
+big_others(uint64_t user)
+{
+    const uint32_t n = __atomic_load_n(&ecm_big_calls.n, __ATOMIC_RELAXED);
+    const uint32_t self = user >= ECM_HYBRID_MIN;
+
+    return n > self ? n - self : 0;
+}
+
 static int
 route_cpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, uint64_t staged)
 {
     if (ctx->engine == ECM_ENGINE_CPU)
         return 1;
-    return route_cpu_q(ctx->k, ctx->isa, user, moved, op, staged, ecd_host_inflight());
+    return route_cpu_q(ctx->k, ctx->isa, user, moved, op, staged, ecd_host_inflight(),
+                       big_others(user));
 }
 
 /* The engine for a host call: 1 = GPU.  `*staged` (in: ECM_STAGED_UNKNOWN)
@@ -736,16 +765,18 @@ static int
 route_gpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op,
           uint64_t (*staged_of)(const void *), const void *arg, uint64_t *staged)
 {
-    int gpu = 0;
+    int gpu = 0, r = 1;
 
     /* the all-mapped GPU estimate is the optimistic one: a call that the CPU
      * wins against it skips the pointer queries (which serialise in the HIP
      * runtime: ~11 us each with 16 calling threads, tools/kbench/ptrq) */
     if (!route_cpu(ctx, user, moved, op, 0)) {
         *staged = staged_of(arg);
-        gpu = !route_cpu(ctx, user, moved, op, *staged);
+        r = route_cpu(ctx, user, moved, op, *staged);
+        gpu = !r;
     }
-    if (ctx->engine == ECM_ENGINE_CPU || ecm_x.always || moved < ecm_x.cpu_below)
+    if (ctx->engine == ECM_ENGINE_CPU || ecm_x.always || moved < ecm_x.cpu_below ||
+        r == ECM_ROUTE_CPU_BUSY)
         return gpu;
     if (gpu) {
         if (obs_explore(ECM_OBS_CPU, op, ctx->k, user))
@@ -768,7 +799,22 @@ ec_method_xover_route(uint32_t k, int32_t op, uint64_t user, uint64_t moved, uin
 {
     if (k < 1 || k > ECM_MAX_K || moved == 0 || (op != ECM_ENCODE && op != ECM_DECODE))
         return -EINVAL;
-    return route_cpu_q(k, ecc_isa_max(), user, moved, op, staged, inflight);
+    return route_cpu_q(k, ecc_isa_max(), user, moved, op, staged, inflight, 0) != 0;
+}
+
+int32_t
+ec_method_xover_plan(uint32_t k, int32_t op, uint64_t user, uint64_t moved, uint64_t staged,
+                     uint64_t inflight, uint32_t others, int32_t *share)
+{
+    int r;
+
+    if (k < 1 || k > ECM_MAX_K || moved == 0 || (op != ECM_ENCODE && op != ECM_DECODE))
+        return -EINVAL;
+    r = route_cpu_q(k, ecc_isa_max(), user, moved, op, staged, inflight, others);
+    if (share)
+        *share = hybrid_share_q(k, ecc_isa_max(), user, moved, op, staged, inflight,
+                                others == 0);
+    return r;
 }
 
 int32_t

@@ -45,6 +45,7 @@ EXPORTS = (
     "ec_method_host_register_async", "ec_method_host_register_flush", "ec_method_buffer_get",
     "ec_method_buffer_put", "ec_method_pool_stats", "ec_method_xover_route",
     "ec_method_xover_split",
+    "ec_method_xover_plan",
     "ec_method_xover_observe", "ec_method_xover_reset", "ec_method_encode_rows",
     "ec_method_encode_rows_device",
 )
@@ -165,6 +166,7 @@ def _load():
         "ec_method_pool_stats": (None, [ctypes.POINTER(PoolStats)]),
         "ec_method_xover_route": (i32, [u32, i32, u64, u64, u64, u64]),
         "ec_method_xover_split": (i32, [u32, i32, u64, u64, u64, u64]),
+        "ec_method_xover_plan": (i32, [u32, i32, u64, u64, u64, u64, u32, ctypes.POINTER(i32)]),
         "ec_method_xover_observe": (i32, [i32, i32, u32, u64, u64]),
         "ec_method_xover_reset": (None, []),
         "ec_method_encode_matrix": (i32, [u32, u32, vp]),

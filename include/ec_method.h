@@ -353,6 +353,17 @@ int32_t ec_method_xover_route(uint32_t k, int32_t op, uint64_t user, uint64_t mo
  * ec_method_xover_route. */
 int32_t ec_method_xover_split(uint32_t k, int32_t op, uint64_t user, uint64_t moved,
                               uint64_t staged, uint64_t inflight);
+/* Both decisions for a call with `others` large (>= 1 MiB) host calls in
+ * flight beside it (r05): returns 0 (a GPU) or nonzero (the CPU engine; 2
+ * when the call stages buffers and its staging copies would take at least the
+ * CPU time coding it on the calling thread takes -- with other callers busy
+ * the GPU route then frees no CPU; EC_STAGE_COPY_GBPS, default 10, is the
+ * copy rate assumed, 0 turns the rule off), and, when `share` is not NULL,
+ * the split share as ec_method_xover_split gives it (staged calls split only
+ * when `others` is 0).  -EINVAL on bad args. */
+int32_t ec_method_xover_plan(uint32_t k, int32_t op, uint64_t user, uint64_t moved,
+                             uint64_t staged, uint64_t inflight, uint32_t others,
+                             int32_t *share);
 int32_t ec_method_xover_observe(int32_t engine, int32_t op, uint32_t k, uint64_t user,
                                 uint64_t ns);
 void ec_method_xover_reset(void);

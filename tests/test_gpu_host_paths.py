@@ -239,6 +239,12 @@ def test_register_errors(ec):
     assert lib.ec_method_host_register(None, 4096) == -22
     assert lib.ec_method_host_register(ctypes.c_void_p(a.ctypes.data), 0) == -22
     assert lib.ec_method_host_unregister(ctypes.c_void_p(a.ctypes.data)) == -22
+    # the refused call's HIP error is reported, not left pending for the
+    # caller's next HIP call (it once failed the next test's torch copy)
+    import torch
+    t = torch.empty(4096, dtype=torch.uint8, device="cuda")
+    t.copy_(torch.from_numpy(a[:4096]))
+    torch.cuda.synchronize()
     with ec.host_registered(a):
         pass
 
@@ -310,3 +316,55 @@ def test_pinned_pages_are_queried_every_call(ec):
     pageable = _attr_queries("pageable")
     assert pinned >= 4 * 7, pinned          # every buffer, every call
     assert pageable <= 7 + 2, pageable      # first call only
+
+
+_MAP_CHILD = r"""
+import mmap, sys
+sys.path[:0] = [%(root)r, %(oracle)r]
+import numpy as np, glusterfs_amd as g, oracle as O
+L = g.ECMatrixList(4, 6)
+data = np.random.default_rng(3).integers(0, 256, 512 * 4 * 8, dtype=np.uint8)
+frags = [np.zeros(512 * 8, np.uint8) for _ in range(6)]
+want = O.encode(4, 6, data)
+for i in range(%(calls)d):
+    if i == %(reg_at)d:      # the library registers memory: cached verdicts go stale
+        m = mmap.mmap(-1, 1 << 20)
+        a = np.frombuffer(m, np.uint8)
+        assert g.ec_method.lib.ec_method_host_register(a.ctypes.data, a.size) == 0
+        assert g.ec_method.lib.ec_method_host_unregister(a.ctypes.data) == 0
+        del a
+    L.encode_batch(8, data, frags)
+    assert all(np.array_equal(f, w) for f, w in zip(frags, want))
+"""
+
+
+def _map_queries(calls, reg_at=-1, ttl_ms="10000"):
+    """hipHostGetDevicePointer ranges checked by `calls` GPU-routed host
+    encodes on 7 pageable buffers (EC_MI355X_DEBUG=1 prints the count)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _MAP_CHILD % dict(root=root, oracle=os.path.join(root, "oracle"), calls=calls,
+                             reg_at=reg_at)
+    env = dict(os.environ, EC_MI355X_DEBUG="1", EC_MI355X_QUIET="1", EC_HOSTPAGE_MS=ttl_ms,
+               EC_GPU_ALWAYS="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stderr.splitlines() if "pointer queries" in l][-1]
+    return int(line.split("attribute,")[1].split()[0])
+
+
+def test_unmapped_ranges_cached_until_a_registration(ec):
+    """ec_device.hip mapped(): a range found not mapped is not asked about
+    again (the queries serialise in the HIP runtime under many client
+    threads) until the lifetime ends or the library registers memory; a
+    mapped verdict is never cached.  Every call is checked against the
+    oracle."""
+    never = _map_queries(20, ttl_ms="0")
+    once = _map_queries(20)
+    again = _map_queries(20, reg_at=10)
+    assert never >= 20 * 7, never
+    assert once <= 2 * 7 + 2, once                 # the first call's ranges only
+    assert again >= once + 7, (once, again)         # asked again after the registration

@@ -119,6 +119,38 @@ assert split(8, DEC, 4 * MiB, infl=1 << 30) == -1
 # (its GPU share would be copied by the CPU threads the other callers need);
 # the probe costs a call that is not alone
 assert split(8, DEC, 4 * MiB, staged_frac=0.25) == -1
+
+# ec_method_xover_plan: both decisions with other large calls in flight
+import ctypes
+def plan(k, op, user, staged_frac=0.0, others=0, infl=0):
+    moved = user * 2 if op == DEC else user + user * (k + 2 * (k // 2)) // k
+    sh = ctypes.c_int32(7)
+    r = L.ec_method_xover_plan(k, op, user, moved, int(moved * staged_frac), infl, others,
+                               ctypes.byref(sh))
+    return r, sh.value
+
+assert L.ec_method_xover_plan(0, DEC, MiB, 2 * MiB, 0, 0, 0, None) < 0
+L.ec_method_xover_reset()
+for _ in range(3):
+    observe(CPU, DEC, 8, 4 * MiB, 13.0)
+    observe(GPAGE, DEC, 8, 4 * MiB, 13.0)
+    observe(GMAP, DEC, 8, 4 * MiB, 13.0)
+# alone: the probes agree, and a staged call may split
+for fr in (0.0, 1.0):
+    r, sh = plan(8, DEC, 4 * MiB, fr)
+    assert r == route(8, DEC, 4 * MiB, fr), (fr, r)
+    assert sh == split(8, DEC, 4 * MiB, fr) if fr == 0.0 else 0 < sh < 1000, (fr, sh)
+# busy: a staged heal window's copies (8 MiB at 10 GB/s) outweigh coding it
+# on the CPU (4 MiB at 13 GB/s): the CPU engine, no split
+assert plan(8, DEC, 4 * MiB, 1.0, others=3) == (2, -1)
+# ...an all-mapped one has no copies: the rule does not apply
+r, sh = plan(8, DEC, 4 * MiB, 0.0, others=3)
+assert r in (0, 1) and sh == split(8, DEC, 4 * MiB), (r, sh)
+# ...nor does it when the CPU engine is slower than the copies (a k = 16
+# decode on a CPU observed at 2 GB/s: 4 MiB of it 2 ms, the copies 0.8 ms)
+for _ in range(6):
+    observe(CPU, DEC, 16, 4 * MiB, 2.0)
+assert plan(16, DEC, 4 * MiB, 1.0, others=3)[0] != 2
 print("OK")
 """
 

@@ -21,7 +21,9 @@
  * Output: one JSON line per (scenario, provenance, way).
  *   gcc -O2 -pthread -Iinclude tools/kbench/concur.c -Lglusterfs_amd/lib \
  *       -lec_mi355x -Wl,-rpath,'$ORIGIN/../../glusterfs_amd/lib' -o tools/kbench/concur
- *   tools/kbench/concur [secs] [gen] [pool|pageable|both]                  */
+ *   tools/kbench/concur [secs] [gen] [pool|pageable|both]
+ *   (CONCUR_HEAL_THREADS: heal threads, default 8; CONCUR_SCEN=heal|write|read:
+ *   that scenario only)                                                   */
 #define _GNU_SOURCE
 #include <pthread.h>
 #include <sched.h>
@@ -253,14 +255,19 @@ int main(int argc, char **argv)
         int scen, threads;
         size_t size;
     } sc[] = {{HEAL, 8, 4u << 20}, {WRITE, 16, 128u << 10}, {READ, 16, 128u << 10}};
+    const char *ht = getenv("CONCUR_HEAL_THREADS");   /* heal threads (default 8) */
+    const char *only = getenv("CONCUR_SCEN");          /* heal | write | read */
+    const int heal_threads = ht && atoi(ht) > 0 ? atoi(ht) : 8;
     const char *which = argc > 3 ? argv[3] : "both";   /* pool | pageable | both */
     for (int pool = 1; pool >= 0; pool--)
         for (size_t s = 0; s < sizeof(sc) / sizeof(sc[0]); s++) {
+            const int threads = sc[s].scen == HEAL ? heal_threads : sc[s].threads;
             if ((pool && !strcmp(which, "pageable")) || (!pool && !strcmp(which, "pool")))
                 continue;
-            bad |= run(&list, "concurrent", sc[s].scen, pool, sc[s].size, sc[s].threads, secs,
-                       mode);
-            bad |= run(&list, "ceiling", sc[s].scen, pool, sc[s].size * sc[s].threads, 1, secs,
+            if (only && strncmp(scen_name[sc[s].scen], only, strlen(only)))
+                continue;
+            bad |= run(&list, "concurrent", sc[s].scen, pool, sc[s].size, threads, secs, mode);
+            bad |= run(&list, "ceiling", sc[s].scen, pool, sc[s].size * threads, 1, secs,
                        mode);
             bad |= run(&list, "serial", sc[s].scen, pool, sc[s].size, 1, secs, mode);
         }
