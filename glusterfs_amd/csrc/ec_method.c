@@ -531,8 +531,12 @@ xover_costs(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t
  * whose copies take at least as much CPU time as coding it on the calling
  * thread would (8+4 heal windows on pageable buffers: copying 2-2.5x the user
  * bytes against a ~7-13 GB/s coder) frees no CPU for them and only adds the
- * trip to the GPU: 8 threads of 4 MiB heal windows on pageable buffers ran
- * 40.6 GB/s auto against 47.7 CPU-only (profiles/r05/r05t_concur.log). */
+ * trip to the GPU.  8 threads of 4 MiB heal windows on pageable buffers ran
+ * 40.6 GB/s auto against 47.7 CPU-only (profiles/r05/r05t_concur.log); most
+ * of that was the buffer-mapping queries (now cached, ec_device.hip
+ * mapped()), and with this rule too the GPU takes ~20 of such calls a second
+ * instead of ~390, within 3 % of the CPU engine alone; pool buffers, which
+ * stage nothing, keep their +12-30 % (profiles/r05/r05w_busyab_*.log). */
 #define ECM_ROUTE_CPU_BUSY 2
 
 static int
