@@ -524,7 +524,7 @@ __device__ __forceinline__ void stage_tile_realign(uint8_t *lds, const EncSrc sr
  * loads that dword itself; it holds the last wanted byte, so no load
  * touches a page the range does not.  Edge stripes (edge buffer) are
  * aligned and take no shift. */
-template <int K, int T, int NW, int P0 = 0>
+template <int K, int T, int NW, int P0 = 0, bool NTL = false>
 __device__ __forceinline__ void stage_tile_shift(uint8_t *lds, const EncSrc src, uint64_t t0,
                                                  uint64_t nstripes, u32 wave, u32 lane)
 {
@@ -554,7 +554,11 @@ __device__ __forceinline__ void stage_tile_shift(uint8_t *lds, const EncSrc src,
             const uint8_t *a = edge ? src.edge + (st == 0 ? 0u : S) + o : src.in + st * S + o;
             sh[it] = edge ? 0u : r_in;
             const u32 *al = reinterpret_cast<const u32 *>(__builtin_assume_aligned(a - sh[it], 4));
-            const v4u v = *reinterpret_cast<const v4u *>(al);
+            v4u v;
+            if constexpr (NTL)
+                v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(al));
+            else
+                v = *reinterpret_cast<const v4u *>(al);
             d[it][0] = v.x;
             d[it][1] = v.y;
             d[it][2] = v.z;
@@ -592,6 +596,9 @@ __device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src
         stage_tile_realign<K, T, NW>(lds, src, t0, nstripes, wave, lane);
     } else if constexpr (SM == 3) {
         stage_tile_shift<K, T, NW>(lds, src, t0, nstripes, wave, lane);
+    } else if constexpr (SM == 7) {
+        /* kb3 A/B: shift staging with non-temporal loads */
+        stage_tile_shift<K, T, NW, 0, true>(lds, src, t0, nstripes, wave, lane);
     } else if constexpr (SM >= 4 && SM <= 6) {
         /* split (kb3 A/B): inputs below KD by LDS-DMA at the caller's
          * alignment (TA-bound), the rest shifted through registers (LDS

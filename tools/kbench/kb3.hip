@@ -685,6 +685,11 @@ int main(int argc, char **argv)
             auto kern4 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 4>;
             auto kern5 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 5>;
             auto kern6 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 6>;
+            auto kern7 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 7>;
+            v.push_back({"shift staging, non-temporal loads (SM=7)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern7, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
             v.push_back({"split: 8 inputs LDS-DMA, 8 shifted (SM=4)", bytes, [=](hipStream_t st) {
                              hipLaunchKernelGGL(kern4, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
                                                 EncSrc{ushift, edge}, f, nst);
@@ -708,6 +713,11 @@ int main(int argc, char **argv)
                          }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
             v.push_back({"tile encoder, dword-aligned shift staging (SM=3)", bytes, [=](hipStream_t st) {
                              hipLaunchKernelGGL(kern3, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            auto kern7 = ec_encode_tile_t<K, N, 4, NW, true, (K == 4), true, 7>;
+            v.push_back({"shift staging, non-temporal loads (SM=7)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern7, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
                                                 EncSrc{ushift, edge}, f, nst);
                          }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
         }
