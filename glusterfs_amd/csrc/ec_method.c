@@ -586,13 +586,79 @@ big_call(uint64_t user, int d)
         __atomic_add_fetch(&ecm_big_calls.n, (uint32_t)d, __ATOMIC_RELAXED);
 }
 
+/* Learned split shares (r05).  The model's share comes from whole-call
+ * estimates; inside a split call the two engines share the host's memory
+ * and the GPU share's latency is the model's constant, so the balance can sit
+ * elsewhere: a single stream of 4 MiB 8+4 heal windows ran 8.1-8.3 GB/s on
+ * pageable buffers at the model's share and 9.6-10.3 at a fixed 35 %, the
+ * fused heal 36.0-37.4 against 39.1-39.7 (profiles/r05/r05aa_sharesweep.log).
+ * So every split call reports how long each share took, from the hand-off to
+ * each engine's end; with C the CPU's time scaled to the whole call, G1 the
+ * GPU's beyond the model's latency L scaled likewise, the share that would
+ * have balanced them is f* = (C - L) / (C + G1), and an exponential average
+ * (weight 1/4; the first sample, a cold start, dropped) of f* per call class
+ * (encode, k-row decode, fewer-row combination), code width, call size and
+ * buffer provenance replaces the model's share once it has a sample.  Its
+ * fixed point is the share at which both engines finish together, whatever
+ * L is.  The model still decides WHETHER to split; the queue ahead on the
+ * GPU moves the learned share as it moves the model's.  EC_XOVER_ADAPT=0
+ * keeps the model's share. */
+enum { ECM_CLS_ENCODE = 0, ECM_CLS_DECODE = 1, ECM_CLS_PART = 2 };
+typedef struct {
+    uint32_t f;      /* share in thousandths, EWMA; 0: no sample yet */
+    uint32_t n;      /* samples seen (the first dropped) */
+    uint32_t pad[14];
+} __attribute__((aligned(64))) ecm_share_t;
+
+static ecm_share_t ecm_share[3][3][ECM_OBS_SIZES][3];
+
+static ecm_share_t *
+share_slot(int cls, uint32_t k, uint64_t user, uint64_t staged, uint64_t moved)
+{
+    return &ecm_share[cls][kbucket(k)][sbucket(user)][gpu_obs_engine(staged, moved) - 1];
+}
+
+/* one split call: `sg` of `n` stripes on the GPU took gpu_ns from the
+ * hand-off, the rest cpu_ns on the calling thread */
+static void
+share_learn(int cls, int op, uint32_t k, int isa, uint64_t user, uint64_t moved,
+            uint64_t staged, uint64_t n, uint64_t sg, uint64_t gpu_ns, uint64_t cpu_ns)
+{
+    ecm_share_t *sl;
+    double c, g, lat, C, G1, f;
+    uint32_t old, upd, fm;
+
+    pthread_once(&ecm_xover_once, xover_init);
+    if (!ecm_x.adapt || ecm_x.hybrid_share || sg == 0 || sg >= n || gpu_ns == 0 || cpu_ns == 0 ||
+        user < ECM_HYBRID_MIN || staged == ECM_STAGED_UNKNOWN)
+        return;
+    sl = share_slot(cls, k, user, staged, moved);
+    if (__atomic_fetch_add(&sl->n, 1, __ATOMIC_RELAXED) == 0)
+        return;
+    xover_costs(k, isa, user, moved, op, staged, 0, &c, &g, &lat);
+    lat *= 1e3;                                             /* ns */
+    C = (double)cpu_ns * (double)n / (double)(n - sg);
+    G1 = ((double)gpu_ns - lat) * (double)n / (double)sg;
+    if (G1 < 0)
+        G1 = 0;
+    f = (C - lat) / (C + G1);
+    f = f < 0.05 ? 0.05 : f > 0.95 ? 0.95 : f;
+    fm = (uint32_t)(f * 1000.0);
+    old = __atomic_load_n(&sl->f, __ATOMIC_RELAXED);
+    do
+        upd = old ? (uint32_t)((int32_t)old + ((int32_t)fm - (int32_t)old) / 4) : fm;
+    while (!__atomic_compare_exchange_n(&sl->f, &old, upd, 1, __ATOMIC_RELAXED,
+                                        __ATOMIC_RELAXED));
+}
+
 /* `alone`: no other large host call is in flight, so a staged GPU share's
- * copies do not compete with other callers' CPU work */
+ * copies do not compete with other callers' CPU work; `cls`: ECM_CLS_* */
 static int
 hybrid_share_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t staged,
-               uint64_t infl, int alone)
+               uint64_t infl, int alone, int cls)
 {
-    double c, g, lat, f;
+    double c, g, lat, f, f0;
+    uint32_t learned;
 
     pthread_once(&ecm_xover_once, xover_init);
     if (!ecm_x.hybrid || ecm_x.always || user < ECM_HYBRID_MIN || moved < ecm_x.cpu_below ||
@@ -612,30 +678,45 @@ hybrid_share_q(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint6
     if (g <= lat || c <= lat)
         return -1;
     f = (c - lat) / (c + g - lat);
-    return f < 0.15 || f > 0.85 ? -1 : (int)(f * 1000.0);
+    if (f < 0.15 || f > 0.85)
+        return -1;
+    learned = ecm_x.adapt ? __atomic_load_n(&share_slot(cls, k, user, staged, moved)->f,
+                                            __ATOMIC_RELAXED)
+                          : 0;
+    if (learned) {
+        f0 = f;
+        if (infl) {             /* the queue's effect, as the model sees it */
+            xover_costs(k, isa, user, moved, op, staged, 0, &c, &g, &lat);
+            f0 = g > lat && c > lat ? (c - lat) / (c + g - lat) : f;
+        }
+        f = (double)learned / 1000.0 + (f - f0);
+        f = f < 0.05 ? 0.05 : f > 0.95 ? 0.95 : f;
+    }
+    return (int)(f * 1000.0);
 }
 
 static int
-hybrid_share(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, uint64_t staged)
+hybrid_share(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, uint64_t staged,
+             int cls)
 {
     if (ctx->engine == ECM_ENGINE_CPU)
         return -1;
     return hybrid_share_q(ctx->k, ctx->isa, user, moved, op, staged, ecd_host_inflight(),
-                          __atomic_load_n(&ecm_big_calls.n, __ATOMIC_RELAXED) <= 1);
+                          __atomic_load_n(&ecm_big_calls.n, __ATOMIC_RELAXED) <= 1, cls);
 }
 
 /* The split share of a call, querying where its buffers live only when an
  * all-mapped call of its size would be split (the queries serialise in the
  * HIP runtime); *staged is filled in when it was queried. */
 static int
-split_share(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op,
+split_share(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op, int cls,
             uint64_t (*staged_of)(const void *), const void *arg, uint64_t *staged)
 {
-    if (hybrid_share(ctx, user, moved, op, 0) <= 0)
+    if (hybrid_share(ctx, user, moved, op, 0, cls) <= 0)
         return -1;
     if (*staged == ECM_STAGED_UNKNOWN)
         *staged = staged_of(arg);
-    return hybrid_share(ctx, user, moved, op, *staged);
+    return hybrid_share(ctx, user, moved, op, *staged, cls);
 }
 
 /* Helper threads that run the GPU share of split calls (at most 8; a call
@@ -645,6 +726,7 @@ typedef struct ecm_task {
     void *arg;
     int rc, done;
     uint64_t ns;                 /* the share's duration */
+    uint64_t t_sub, wall;        /* hand-off time; done - hand-off */
     char err[256];               /* its error text when it failed */
     struct ecm_task *next;
 } ecm_task_t;
@@ -681,6 +763,7 @@ helper_main(void *unused)
         t0 = now_ns();
         rc = t->fn(t->arg);
         t->ns = now_ns() - t0;
+        t->wall = t0 + t->ns - t->t_sub;
         t->err[0] = 0;
         if (rc && ecd_error_seq() != seq)
             snprintf(t->err, sizeof t->err, "%s", ecd_last_error());
@@ -702,6 +785,7 @@ helper_submit(ecm_task_t *t)
 
     t->done = 0;
     t->next = NULL;
+    t->t_sub = now_ns();
     pthread_mutex_lock(&ecm_pool_mu);
     if (ecm_helpers_idle <= ecm_q_len) {
         ok = ecm_helpers < ECM_HELPERS_MAX && pthread_attr_init(&at) == 0;
@@ -817,8 +901,22 @@ ec_method_xover_plan(uint32_t k, int32_t op, uint64_t user, uint64_t moved, uint
     r = route_cpu_q(k, ecc_isa_max(), user, moved, op, staged, inflight, others);
     if (share)
         *share = hybrid_share_q(k, ecc_isa_max(), user, moved, op, staged, inflight,
-                                others == 0);
+                                others == 0, op);
     return r;
+}
+
+int32_t
+ec_method_xover_observe_split(int32_t op, uint32_t k, uint64_t user, uint64_t moved,
+                              uint64_t staged, uint32_t gpu_share, uint64_t gpu_ns,
+                              uint64_t cpu_ns)
+{
+    const uint64_t n = 1000;
+
+    if (k < 1 || k > ECM_MAX_K || moved == 0 || (op != ECM_ENCODE && op != ECM_DECODE) ||
+        gpu_share == 0 || gpu_share >= 1000)
+        return -EINVAL;
+    share_learn(op, op, k, ecc_isa_max(), user, moved, staged, n, gpu_share, gpu_ns, cpu_ns);
+    return 0;
 }
 
 int32_t
@@ -827,7 +925,7 @@ ec_method_xover_split(uint32_t k, int32_t op, uint64_t user, uint64_t moved, uin
 {
     if (k < 1 || k > ECM_MAX_K || moved == 0 || (op != ECM_ENCODE && op != ECM_DECODE))
         return -EINVAL;
-    return hybrid_share_q(k, ecc_isa_max(), user, moved, op, staged, inflight, 0);
+    return hybrid_share_q(k, ecc_isa_max(), user, moved, op, staged, inflight, 0, op);
 }
 
 int32_t
@@ -849,12 +947,17 @@ void
 ec_method_xover_reset(void)
 {
     ecm_obs_t *o = &ecm_obs[0][0][0][0];
+    ecm_share_t *sh = &ecm_share[0][0][0][0];
     size_t i;
 
     for (i = 0; i < sizeof(ecm_obs) / sizeof(ecm_obs[0][0][0][0]); i++) {
         __atomic_store_n(&o[i].kbps, 0, __ATOMIC_RELAXED);
         __atomic_store_n(&o[i].lost, 0, __ATOMIC_RELAXED);
         __atomic_store_n(&o[i].n, 0, __ATOMIC_RELAXED);
+    }
+    for (i = 0; i < sizeof(ecm_share) / sizeof(ecm_share[0][0][0][0]); i++) {
+        __atomic_store_n(&sh[i].f, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&sh[i].n, 0, __ATOMIC_RELAXED);
     }
 }
 
@@ -1445,7 +1548,7 @@ encode_split(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out
     const uint64_t S = (uint64_t)ctx->k * EC_METHOD_CHUNK_SIZE, user = nstripes * S;
     const uint64_t sg = split_stripes(nstripes, share, 1);
     struct enc_share es = {ctx, sg, in, out};
-    ecm_task_t t = {enc_share_gpu, &es, 0, 0, 0, "", NULL};
+    ecm_task_t t = {enc_share_gpu, &es, 0, 0, 0, 0, 0, "", NULL};
     uint8_t *o2[ECM_MAX_N];
     uint64_t t0;
     uint32_t i;
@@ -1456,13 +1559,17 @@ encode_split(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out
         o2[i] = (uint8_t *)out[i] + sg * EC_METHOD_CHUNK_SIZE;
     t0 = now_ns();
     ecc_encode(ctx->isa, ctx->k, ctx->n, nstripes - sg, (const uint8_t *)in + sg * S, o2);
-    obs_record_part(ECM_OBS_CPU, ECM_ENCODE, ctx->k, user, (nstripes - sg) * S, now_ns() - t0);
+    t0 = now_ns() - t0;
+    obs_record_part(ECM_OBS_CPU, ECM_ENCODE, ctx->k, user, (nstripes - sg) * S, t0);
     stat_add(ECM_STAT_CPU);
     helper_wait(&t);
     if (t.rc == 0) {
+        const uint64_t moved = nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n);
+
         stat_add(ECM_STAT_GPU);
-        obs_record_part(gpu_obs_engine(staged, nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n)),
-                        ECM_ENCODE, ctx->k, user, sg * S, t.ns);
+        obs_record_part(gpu_obs_engine(staged, moved), ECM_ENCODE, ctx->k, user, sg * S, t.ns);
+        share_learn(ECM_CLS_ENCODE, ECM_ENCODE, ctx->k, ctx->isa, user, moved, staged, nstripes,
+                    sg, t.wall, t0);
         return 0;
     }
     if (t.err[0])
@@ -1483,7 +1590,7 @@ host_encode_1(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *ou
     int rc, gpu, share;
 
     gpu = route_gpu(ctx, user, bytes, ECM_ENCODE, enc_staged, &eb, &staged);
-    share = split_share(ctx, user, bytes, ECM_ENCODE, enc_staged, &eb, &staged);
+    share = split_share(ctx, user, bytes, ECM_ENCODE, ECM_CLS_ENCODE, enc_staged, &eb, &staged);
     if (share > 0 && (rc = encode_split(ctx, nstripes, in, out, share, staged)) != -EAGAIN)
         return rc;
     if (gpu) {
@@ -1600,7 +1707,7 @@ decode_split(ecm_ctx_t *ctx, const struct dec_call *c, int share, uint64_t stage
     const uint64_t sg = split_stripes(c->nstripes, share, unit);
     const uint64_t per = (uint64_t)c->k * EC_METHOD_CHUNK_SIZE, user = c->nstripes * per;
     struct dec_call g = *c;
-    ecm_task_t t = {dec_share_gpu, &g, 0, 0, 0, "", NULL};
+    ecm_task_t t = {dec_share_gpu, &g, 0, 0, 0, 0, 0, "", NULL};
     uint64_t t0;
     int rc;
 
@@ -1609,16 +1716,20 @@ decode_split(ecm_ctx_t *ctx, const struct dec_call *c, int share, uint64_t stage
         return -EAGAIN;
     t0 = now_ns();
     rc = cpu_decode(ctx, c, sg, c->nstripes);
+    t0 = now_ns() - t0;
     if (rc == 0) {
-        obs_record_part(ECM_OBS_CPU, ECM_DECODE, c->k, user, (c->nstripes - sg) * per,
-                        now_ns() - t0);
+        obs_record_part(ECM_OBS_CPU, ECM_DECODE, c->k, user, (c->nstripes - sg) * per, t0);
         stat_add(ECM_STAT_CPU);
     }
     helper_wait(&t);
     if (t.rc == 0) {
+        const uint64_t moved = c->nstripes * EC_METHOD_CHUNK_SIZE * (c->k + c->rows);
+
         stat_add(ECM_STAT_GPU);
-        obs_record_part(gpu_obs_engine(staged, c->nstripes * EC_METHOD_CHUNK_SIZE * (c->k + c->rows)),
-                        ECM_DECODE, c->k, user, sg * per, t.ns);
+        obs_record_part(gpu_obs_engine(staged, moved), ECM_DECODE, c->k, user, sg * per, t.ns);
+        if (rc == 0)
+            share_learn(c->rows == c->k ? ECM_CLS_DECODE : ECM_CLS_PART, ECM_DECODE, c->k,
+                        ctx->isa, user, moved, staged, c->nstripes, sg, t.wall, t0);
         return rc;
     }
     if (t.err[0])
@@ -1643,7 +1754,8 @@ host_decode_1(ecm_ctx_t *ctx, uint32_t k, uint32_t rows, uint64_t nstripes, uint
     int rc, gpu, share;
 
     gpu = route_gpu(ctx, fl * k, bytes, ECM_DECODE, dec_staged, &db, &staged);
-    share = split_share(ctx, fl * k, bytes, ECM_DECODE, dec_staged, &db, &staged);
+    share = split_share(ctx, fl * k, bytes, ECM_DECODE,
+                        rows == k ? ECM_CLS_DECODE : ECM_CLS_PART, dec_staged, &db, &staged);
     if (share > 0 && (rc = decode_split(ctx, &call, share, staged)) != -EAGAIN)
         return rc;
     if (gpu) {
@@ -1832,19 +1944,25 @@ host_encode_rows_1(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, uint32_t m
     int rc, share;
 
     /* a near tie: the GPU takes the first share, the CPU the rest */
-    share = split_share(ctx, user, bytes, ECM_DECODE, enc_staged, &eb, &staged);
+    share = split_share(ctx, user, bytes, ECM_DECODE, ECM_CLS_PART, enc_staged, &eb, &staged);
     sg = share > 0 ? split_stripes(nstripes, share, 1) : 0;
     if (sg) {
         struct rows_share rs = {ctx, sg, in, m, outs, pat};
-        ecm_task_t t = {rows_share_gpu, &rs, 0, 0, 0, "", NULL};
+        ecm_task_t t = {rows_share_gpu, &rs, 0, 0, 0, 0, 0, "", NULL};
 
         if (helper_submit(&t) == 0) {
+            uint64_t t0 = now_ns();
+
             rc = cpu_encode_rows(ctx, sg, nstripes, in, m, outs, pat);
+            t0 = now_ns() - t0;
             if (rc == 0)
                 stat_add(ECM_STAT_CPU);
             helper_wait(&t);
             if (t.rc == 0) {
                 stat_add(ECM_STAT_GPU);
+                if (rc == 0)
+                    share_learn(ECM_CLS_PART, ECM_DECODE, ctx->k, ctx->isa, user, bytes, staged,
+                                nstripes, sg, t.wall, t0);
                 return rc;
             }
             if (t.err[0])

@@ -46,6 +46,7 @@ EXPORTS = (
     "ec_method_buffer_put", "ec_method_pool_stats", "ec_method_xover_route",
     "ec_method_xover_split",
     "ec_method_xover_plan",
+    "ec_method_xover_observe_split",
     "ec_method_xover_observe", "ec_method_xover_reset", "ec_method_encode_rows",
     "ec_method_encode_rows_device",
 )
@@ -167,6 +168,7 @@ def _load():
         "ec_method_xover_route": (i32, [u32, i32, u64, u64, u64, u64]),
         "ec_method_xover_split": (i32, [u32, i32, u64, u64, u64, u64]),
         "ec_method_xover_plan": (i32, [u32, i32, u64, u64, u64, u64, u32, ctypes.POINTER(i32)]),
+        "ec_method_xover_observe_split": (i32, [i32, u32, u64, u64, u64, u32, u64, u64]),
         "ec_method_xover_observe": (i32, [i32, i32, u32, u64, u64]),
         "ec_method_xover_reset": (None, []),
         "ec_method_encode_matrix": (i32, [u32, u32, vp]),

@@ -364,6 +364,16 @@ int32_t ec_method_xover_split(uint32_t k, int32_t op, uint64_t user, uint64_t mo
 int32_t ec_method_xover_plan(uint32_t k, int32_t op, uint64_t user, uint64_t moved,
                              uint64_t staged, uint64_t inflight, uint32_t others,
                              int32_t *share);
+/* A split call as the library records one (r05, tests): `gpu_share` per
+ * mille of the call's stripes took `gpu_ns` on a GPU from the hand-off, the
+ * rest `cpu_ns` on the CPU engine.  The share later calls of this class,
+ * width, size and provenance get moves toward the one that would have
+ * balanced the two (ec_method.c share_learn; the first sample of a slot is
+ * a cold start and dropped; ec_method_xover_reset forgets them).  -EINVAL on
+ * bad args. */
+int32_t ec_method_xover_observe_split(int32_t op, uint32_t k, uint64_t user, uint64_t moved,
+                                      uint64_t staged, uint32_t gpu_share, uint64_t gpu_ns,
+                                      uint64_t cpu_ns);
 int32_t ec_method_xover_observe(int32_t engine, int32_t op, uint32_t k, uint64_t user,
                                 uint64_t ns);
 void ec_method_xover_reset(void);

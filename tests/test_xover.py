@@ -151,6 +151,38 @@ assert r in (0, 1) and sh == split(8, DEC, 4 * MiB), (r, sh)
 for _ in range(6):
     observe(CPU, DEC, 16, 4 * MiB, 2.0)
 assert plan(16, DEC, 4 * MiB, 1.0, others=3)[0] != 2
+
+# learned split shares: a split whose GPU share took twice the CPU share's
+# time moves later shares of that class toward the balance, and not others
+L.ec_method_xover_reset()
+for _ in range(3):
+    observe(CPU, DEC, 8, 4 * MiB, 13.0)
+    observe(GMAP, DEC, 8, 4 * MiB, 13.0)
+    observe(CPU, ENC, 8, 4 * MiB, 13.0)
+    observe(GMAP, ENC, 8, 4 * MiB, 13.0)
+m0 = split(8, DEC, 4 * MiB)
+e0 = split(8, ENC, 4 * MiB)
+mv = 2 * 4 * MiB
+assert L.ec_method_xover_observe_split(DEC, 8, 4 * MiB, mv, 0, 0, 1, 1) < 0
+assert L.ec_method_xover_observe_split(DEC, 8, 4 * MiB, mv, 0, 500, 400000, 200000) == 0
+assert split(8, DEC, 4 * MiB) == m0                   # the first sample is a cold start
+seq = []
+for _ in range(12):
+    sh = split(8, DEC, 4 * MiB)
+    # an engine pair where the GPU codes at half the CPU's rate (+30 us):
+    # each share's time follows from the share taken
+    gpu_ns = int(30000 + sh / 1000 * 600000)
+    cpu_ns = int((1 - sh / 1000) * 300000)
+    assert L.ec_method_xover_observe_split(DEC, 8, 4 * MiB, mv, 0, sh, gpu_ns, cpu_ns) == 0
+    seq.append(split(8, DEC, 4 * MiB))
+# balance: 30 + 600 f = 300 (1 - f) -> f = 0.30
+assert abs(seq[-1] - 300) <= 15, seq
+assert seq[0] < m0, (m0, seq)
+assert split(8, ENC, 4 * MiB) == e0                   # encode slots untouched
+# a queue ahead on the GPU still shrinks the learned share
+assert split(8, DEC, 4 * MiB, infl=4 * MiB) < seq[-1]
+L.ec_method_xover_reset()
+assert split(8, DEC, 4 * MiB) != seq[-1] or m0 == seq[-1]
 print("OK")
 """
 
