@@ -329,7 +329,7 @@ env_u64(const char *name, uint64_t dflt)
 
 static struct {
     uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, page_gbps_l, always;
-    uint64_t adapt, hybrid, hybrid_share, copy_gbps;
+    uint64_t adapt, hybrid, hybrid_share, copy_gbps, spin_ns;
 } __attribute__((aligned(64))) ecm_x;
 static pthread_once_t ecm_xover_once __attribute__((aligned(64))) = PTHREAD_ONCE_INIT;
 
@@ -353,6 +353,9 @@ xover_init(void)
     /* one CPU thread's copy rate between pageable and pinned memory (the
      * staging copies of a GPU call with pageable buffers); 0: no busy rule */
     ecm_x.copy_gbps = env_u64("EC_STAGE_COPY_GBPS", 10);
+    /* how long an idle split-call helper polls for the next share before it
+     * sleeps (a woken thread takes tens of us to run again) */
+    ecm_x.spin_ns = env_u64("EC_HELPER_SPIN_US", 0) * 1000;
 }
 
 enum { ECM_ENCODE = 0, ECM_DECODE = 1 };
@@ -629,7 +632,7 @@ share_learn(int cls, int op, uint32_t k, int isa, uint64_t user, uint64_t moved,
     uint32_t old, upd, fm;
 
     pthread_once(&ecm_xover_once, xover_init);
-    if (!ecm_x.adapt || ecm_x.hybrid_share || sg == 0 || sg >= n || gpu_ns == 0 || cpu_ns == 0 ||
+    if (!ecm_x.adapt || sg == 0 || sg >= n || gpu_ns == 0 || cpu_ns == 0 ||
         user < ECM_HYBRID_MIN || staged == ECM_STAGED_UNKNOWN)
         return;
     sl = share_slot(cls, k, user, staged, moved);
@@ -746,10 +749,23 @@ helper_main(void *unused)
     int rc;
 
     (void)unused;
+    pthread_once(&ecm_xover_once, xover_init);
     pthread_mutex_lock(&ecm_pool_mu);
     for (;;) {
         while (!ecm_q_head) {
             ecm_helpers_idle++;
+            if (ecm_x.spin_ns) {
+                const uint64_t end = now_ns() + ecm_x.spin_ns;
+
+                pthread_mutex_unlock(&ecm_pool_mu);
+                while (__atomic_load_n(&ecm_q_len, __ATOMIC_RELAXED) == 0 && now_ns() < end)
+                    __builtin_ia32_pause();
+                pthread_mutex_lock(&ecm_pool_mu);
+                if (ecm_q_head) {
+                    ecm_helpers_idle--;
+                    break;
+                }
+            }
             pthread_cond_wait(&ecm_pool_cv, &ecm_pool_mu);
             ecm_helpers_idle--;
         }
@@ -757,7 +773,7 @@ helper_main(void *unused)
         ecm_q_head = t->next;
         if (!ecm_q_head)
             ecm_q_tail = &ecm_q_head;
-        ecm_q_len--;
+        __atomic_sub_fetch(&ecm_q_len, 1, __ATOMIC_RELAXED);
         pthread_mutex_unlock(&ecm_pool_mu);
         seq = ecd_error_seq();
         t0 = now_ns();
@@ -800,7 +816,7 @@ helper_submit(ecm_task_t *t)
     if (ok) {
         *ecm_q_tail = t;
         ecm_q_tail = &t->next;
-        ecm_q_len++;
+        __atomic_add_fetch(&ecm_q_len, 1, __ATOMIC_RELAXED);
         pthread_cond_signal(&ecm_pool_cv);
     }
     pthread_mutex_unlock(&ecm_pool_mu);
