@@ -573,6 +573,7 @@ def heal_sweep(mode, windows=64):
                 data, frs, out, eo = bufs[0]              # warm (lazy setup)
                 heal_window(frs, out, eo)
                 st0 = g.stats()
+                cs0 = cpu_stat()
                 td, te = [], []
                 t0 = time.perf_counter()
                 for i in range(windows):
@@ -583,6 +584,17 @@ def heal_sweep(mode, windows=64):
                     td.append(b - a)
                 el = time.perf_counter() - t0
                 st1 = g.stats()
+                throttled = cpu_stat_delta(cs0)
+                # the split shares the library settled on for this provenance
+                # (per mille, -1: not split), decode and re-encode
+                import ctypes
+                shares = {}
+                ps = {"pageable": 1.0, "registered": 0.0, "ec_provenance_calloc": 0.5}.get(prov, 0.0)
+                for name, op, moved in (("decode", 1, 2 * W), ("encode", 0, W + n * fl)):
+                    sh = ctypes.c_int32(-2)
+                    lib.ec_method_xover_plan(k, op, W, moved, int(moved * ps), 0, 0,
+                                             ctypes.byref(sh))
+                    shares[name] = sh.value
                 ok = (fused or all(np.array_equal(o, d) for d, _, o, _ in bufs)) and all(
                     np.array_equal(e[i], f[i]) for _, f, _, e in bufs for i in range(n)
                     if (sel >> i) & 1)
@@ -597,6 +609,10 @@ def heal_sweep(mode, windows=64):
                  encode_us_median=round(sorted(te)[len(te) // 2] * 1e6, 1),
                  gpu_calls=st1["gpu_calls"] - st0["gpu_calls"],
                  cpu_calls=st1["cpu_calls"] - st0["cpu_calls"])
+        if mode == "auto" and prov not in ("ec_provenance_rows", "ec_provenance_fused"):
+            r["split_share_permille"] = shares
+        if throttled:
+            r["cgroup_throttled"] = throttled
         dreg = ps1["deferred_registers"] - ps0["deferred_registers"]
         if dreg:
             r["arena_register_us_per_2MiB"] = round(

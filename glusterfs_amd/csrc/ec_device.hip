@@ -1030,10 +1030,19 @@ struct Stage {
 std::mutex g_pool_mu;
 std::vector<Stage *> g_pool[kMaxDev];
 
+/* Staging slots hold at most one batch of the call (never more than its
+ * data), so their size follows the call.  They grow to the next power of two:
+ * a split call's GPU share (ec_method.c) varies from call to call, and slots
+ * sized to each new largest share were freed and re-pinned every time the
+ * share set a new high -- unregistering, mapping, faulting in and
+ * registering MiBs of memory inside the call (a single stream of pageable
+ * 4 MiB heal windows ran 4.2-10.8 GB/s from run to run). */
 int grow(uint8_t *(&slot)[kSlots], size_t &cap, size_t want, int dev)
 {
     if (want <= cap)
         return 0;
+    if (want < ((size_t)1 << 62))
+        want = (size_t)1 << (64 - __builtin_clzll((unsigned long long)want - 1));
     for (auto &p : slot)
         if (p) {
             pinned_free(p);

@@ -329,7 +329,7 @@ env_u64(const char *name, uint64_t dflt)
 
 static struct {
     uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, page_gbps_l, always;
-    uint64_t adapt, hybrid, hybrid_share, copy_gbps, spin_ns;
+    uint64_t adapt, hybrid, hybrid_share, copy_gbps, spin_ns, learn;
 } __attribute__((aligned(64))) ecm_x;
 static pthread_once_t ecm_xover_once __attribute__((aligned(64))) = PTHREAD_ONCE_INIT;
 
@@ -356,6 +356,7 @@ xover_init(void)
     /* how long an idle split-call helper polls for the next share before it
      * sleeps (a woken thread takes tens of us to run again) */
     ecm_x.spin_ns = env_u64("EC_HELPER_SPIN_US", 0) * 1000;
+    ecm_x.learn = env_u64("EC_SPLIT_LEARN", 1);   /* 0: the model's split shares (A/B) */
 }
 
 enum { ECM_ENCODE = 0, ECM_DECODE = 1 };
@@ -605,7 +606,7 @@ big_call(uint64_t user, int d)
  * fixed point is the share at which both engines finish together, whatever
  * L is.  The model still decides WHETHER to split; the queue ahead on the
  * GPU moves the learned share as it moves the model's.  EC_XOVER_ADAPT=0
- * keeps the model's share. */
+ * or EC_SPLIT_LEARN=0 keeps the model's share. */
 enum { ECM_CLS_ENCODE = 0, ECM_CLS_DECODE = 1, ECM_CLS_PART = 2 };
 typedef struct {
     uint32_t f;      /* share in thousandths, EWMA; 0: no sample yet */
@@ -632,7 +633,7 @@ share_learn(int cls, int op, uint32_t k, int isa, uint64_t user, uint64_t moved,
     uint32_t old, upd, fm;
 
     pthread_once(&ecm_xover_once, xover_init);
-    if (!ecm_x.adapt || sg == 0 || sg >= n || gpu_ns == 0 || cpu_ns == 0 ||
+    if (!ecm_x.adapt || !ecm_x.learn || sg == 0 || sg >= n || gpu_ns == 0 || cpu_ns == 0 ||
         user < ECM_HYBRID_MIN || staged == ECM_STAGED_UNKNOWN)
         return;
     sl = share_slot(cls, k, user, staged, moved);

@@ -44,6 +44,8 @@ for step in "$@"; do
     busyab) run busyab 600 bash -c 'for r in 1 2; do for t in ${BUSY_THREADS:-2 4 8}; do for c in 0 10; do echo "== round $r threads $t EC_STAGE_COPY_GBPS=$c"; EC_GPU_ALWAYS=0 EC_STAGE_COPY_GBPS=$c CONCUR_HEAL_THREADS=$t CONCUR_SCEN=heal tools/kbench/concur 1 auto ${BUSY_BUFS:-pageable} || exit 1; done; echo "== round $r threads $t cpu"; EC_GPU_ALWAYS=0 CONCUR_HEAL_THREADS=$t CONCUR_SCEN=heal tools/kbench/concur 1 avx ${BUSY_BUFS:-pageable} || exit 1; done; done' ;;
     sharesweep) run sharesweep 900 bash -c 'for r in 1 2; do for f in ${SHARES:-0 350 450 550 650}; do echo "== round $r EC_HYBRID_SHARE=$f"; EC_GPU_ALWAYS=0 EC_HYBRID_SHARE=$f python3 bench.py --heal-sweep auto --steps 256 || exit 1; done; done' ;;
     spinab) run spinab 900 bash -c 'for r in 1 2; do for u in ${SPINS:-0 50 200}; do echo "== round $r EC_HELPER_SPIN_US=$u"; EC_GPU_ALWAYS=0 EC_HELPER_SPIN_US=$u python3 bench.py --heal-sweep auto --steps 256 || exit 1; done; done' ;;
+    hsauto) run hsauto 900 bash -c 'for r in ${HS_ROUNDS:-1 2 3}; do echo "== round $r"; EC_GPU_ALWAYS=0 python3 bench.py --heal-sweep auto --steps 256 || exit 1; done' ;;
+    learnab) run learnab 900 bash -c 'for r in ${HS_ROUNDS:-1 2}; do for l in 0 1; do echo "== round $r EC_SPLIT_LEARN=$l"; EC_GPU_ALWAYS=0 EC_SPLIT_LEARN=$l python3 bench.py --heal-sweep auto --steps 256 || exit 1; done; done' ;;
     ablib) run ablib 900 bash tools/ab_lib.sh "${AB_ARGS:-mixed:8+4 1 mixed:16+4:64 1 dec:8+4:FF0 1}" ;;
     hsweep3) run hsweep3 400 bash -c 'for m in auto gpu cpu; do echo "== $m"; if [ $m = gpu ]; then E=1; else E=0; fi; EC_GPU_ALWAYS=$E python3 bench.py --heal-sweep $m --steps 256 || exit 1; done' ;;
     kb3) run kb3 600 tools/kbench/kb3 ${KB3_ARGS:-1 7 all} ;;
