@@ -152,3 +152,56 @@ print("OK")
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=200)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_learned_shares_stay_exact():
+    """Split calls without a fixed share: the library learns each class's
+    share from the two shares' times (ec_method.c share_learn), so the split
+    point moves from call to call; every result must stay bit-exact, and the
+    learned share must be a real split."""
+    env = dict(os.environ)
+    env.pop("EC_GPU_ALWAYS", None)
+    env.update(EC_CPU_ENC_GBPS_K2="60", EC_CPU_DEC_GBPS_K="60", EC_MI355X_QUIET="1")
+    env.pop("EC_HYBRID_SHARE", None)
+    code = r"""
+import ctypes, sys
+sys.path[:0] = [%(root)r, %(oracle)r]
+import numpy as np
+import torch  # noqa: F401
+import glusterfs_amd as g
+import oracle as O
+k, n = 8, 12
+nst = (4 << 20) // (512 * k)
+rng = np.random.default_rng(11)
+splits = 0
+with g.ECMatrixList(k, n) as L:
+    keep = []
+    def pinned(nb):
+        p = g.PinnedArray(nb)
+        keep.append(p)
+        return p.array[:nb]
+    data = pinned(512 * k * nst)
+    frags = [pinned(512 * nst) for _ in range(n)]
+    out = pinned(512 * k * nst)
+    rows = list(range(5, 13))
+    mask = sum(1 << (r - 1) for r in rows)
+    for it in range(24):
+        data[:] = rng.integers(0, 256, data.size, dtype=np.uint8)
+        s0 = g.stats()
+        L.encode_batch(nst, data, frags)
+        want = O.encode(k, n, np.array(data), nthreads=8)
+        assert all(np.array_equal(f, w) for f, w in zip(frags, want)), ("encode", it)
+        L.decode_batch(nst, mask, rows, [frags[r - 1] for r in rows], out)
+        assert np.array_equal(out, data), ("decode", it)
+        s1 = g.stats()
+        splits += (s1["gpu_calls"] - s0["gpu_calls"]) > 0 and (s1["cpu_calls"] - s0["cpu_calls"]) > 0
+    sh = ctypes.c_int32(-2)
+    g.ec_method.lib.ec_method_xover_plan(k, 1, data.size, 2 * data.size, 0, 0, 0, ctypes.byref(sh))
+print("splits", splits, "share", sh.value)
+assert splits >= 8, splits
+print("OK")
+""" % dict(root=ROOT, oracle=os.path.join(ROOT, "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=280)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+    print(r.stdout.strip().splitlines()[-2])
