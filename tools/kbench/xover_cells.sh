@@ -20,7 +20,7 @@ for k in ${KS:-4 8 16}; do
             auto) ENV=""; GEN=auto ;;
           esac
           printf "%-4s " $mode >> "$OUT"
-          env $ENV EC_MI355X_QUIET=1 timeout -k 10 60 tools/kbench/smallcalls ${SECS:-0.5} $k $dec ${REG:-0} $kib $thr $GEN \
+          env $ENV EC_MI355X_QUIET=1 timeout -k 10 60 ${SMALLCALLS:-tools/kbench/smallcalls} ${SECS:-0.5} $k $dec ${REG:-0} $kib $thr $GEN \
             2>/dev/null | grep thr: >> "$OUT" || exit 1
         done
       done
