@@ -36,6 +36,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -428,6 +429,9 @@ void add_gather(std::vector<CopyPool::Piece> &v, uint8_t *dst, const std::vector
  * accesses. */
 bool pool_owns(const void *p, size_t n);
 
+bool user_range_live(const void *p, size_t n);
+bool numa_alloc_live(const void *p, size_t n);
+
 /* Ranges found NOT mapped, per thread (direct-mapped on the start page).
  * The two hipHostGetDevicePointer queries of a range serialise in the HIP
  * runtime like the attribute queries (ecd_ptr_device, below): a pageable
@@ -450,7 +454,13 @@ uint8_t *mapped(const void *p, size_t n)
 {
     if (!p || ((uintptr_t)p & 15))
         return nullptr;
-    if (pool_owns(p, n))   /* a pool buffer: registered at the same address */
+    /* the library's own mappings -- a pool buffer, a range registered
+     * through ec_method_host_register[_async], ec_method_host_alloc memory --
+     * are known without asking the HIP runtime, whose queries serialise
+     * across threads (~11 us each with 16 callers, tools/kbench/ptrq) and
+     * cannot be cached for mapped memory (above): registered at the same
+     * address, live until their owner unregisters or frees them */
+    if (pool_owns(p, n) || user_range_live(p, n) || numa_alloc_live(p, n))
         return static_cast<uint8_t *>(const_cast<void *>(p));
     const uint64_t ttl = hostpage_ttl_ns();
     const uintptr_t pg = (uintptr_t)p >> 12;
@@ -531,6 +541,17 @@ int device_numa(int dev)
  * Node < 0, or any step failing: hipHostMalloc. */
 std::mutex g_numa_mu;
 std::map<void *, size_t> g_numa_allocs;
+
+bool numa_alloc_live(const void *p, size_t n)
+{
+    std::lock_guard<std::mutex> g(g_numa_mu);
+    auto it = g_numa_allocs.upper_bound(const_cast<void *>(p));
+    if (it == g_numa_allocs.begin())
+        return false;
+    --it;
+    const uintptr_t b = (uintptr_t)it->first, a = (uintptr_t)p;
+    return a >= b && a + n <= b + it->second;
+}
 
 void *pinned_alloc(size_t bytes, int node)
 {
@@ -839,15 +860,37 @@ class RangeSet {
     {
         const uintptr_t s = (uintptr_t)p & ~kPageMask;
         const uintptr_t e = ((uintptr_t)p + n + kPageMask) & ~kPageMask;
-        std::lock_guard<std::mutex> g(mu_);
+        std::unique_lock<std::shared_mutex> g(mu_);
         auto it = by_start_.lower_bound(s);
         if (it != by_start_.end() && it->first < e)
             return false;
-        if (it != by_start_.begin() && std::prev(it)->second.first > s)
+        if (it != by_start_.begin() && std::prev(it)->second.e > s)
             return false;
-        by_start_[s] = {e, (uintptr_t)p};
+        by_start_[s] = Range{e, (uintptr_t)p, (uintptr_t)p + n, false};
         start_of_[(uintptr_t)p] = s;
         return true;
+    }
+
+    /* p's registration succeeded: its range is mapped from now on */
+    void mark_ready(const void *p)
+    {
+        std::unique_lock<std::shared_mutex> g(mu_);
+        const auto it = start_of_.find((uintptr_t)p);
+        if (it != start_of_.end())
+            by_start_[it->second].ready = true;
+    }
+
+    /* [q, q + n) lies inside one range whose registration has succeeded and
+     * that its owner has not unregistered: mapped, at the same address */
+    bool live(const void *q, size_t n)
+    {
+        const uintptr_t a = (uintptr_t)q;
+        std::shared_lock<std::shared_mutex> g(mu_);
+        auto it = by_start_.upper_bound(a);
+        if (it == by_start_.begin())
+            return false;
+        const Range &r = std::prev(it)->second;
+        return r.ready && a >= r.p && a + n <= r.end;
     }
 
     /* Drop the reservation of p.  Returns false when p's registration had
@@ -856,7 +899,7 @@ class RangeSet {
      * at the same start address. */
     bool release(const void *p)
     {
-        std::lock_guard<std::mutex> g(mu_);
+        std::unique_lock<std::shared_mutex> g(mu_);
         const auto it = start_of_.find((uintptr_t)p);
         if (it == start_of_.end())
             return true;
@@ -869,15 +912,20 @@ class RangeSet {
      * other registration can take its pages) until its owner unregisters. */
     void mark_failed(const void *p)
     {
-        std::lock_guard<std::mutex> g(mu_);
+        std::unique_lock<std::shared_mutex> g(mu_);
         if (start_of_.count((uintptr_t)p))
             failed_.insert((uintptr_t)p);
     }
 
   private:
     static constexpr uintptr_t kPageMask = 4095;
-    std::mutex mu_;
-    std::map<uintptr_t, std::pair<uintptr_t, uintptr_t>> by_start_; /* s -> (e, p) */
+    struct Range {
+        uintptr_t e;      /* page-rounded end */
+        uintptr_t p, end; /* the registered bytes */
+        bool ready;       /* registered (a deferred one: done) */
+    };
+    std::shared_mutex mu_;
+    std::map<uintptr_t, Range> by_start_;                            /* s -> range */
     std::map<uintptr_t, uintptr_t> start_of_;                        /* p -> s */
     std::set<uintptr_t> failed_;                                     /* p       */
 };
@@ -886,6 +934,11 @@ RangeSet &user_ranges()
 {
     static RangeSet *r = new RangeSet;
     return *r;
+}
+
+bool user_range_live(const void *p, size_t n)
+{
+    return user_ranges().live(p, n);
 }
 
 /* ec_method_host_register_async: GlusterFS calls the arena hook from
@@ -976,6 +1029,7 @@ class RegQueue {
                                     "buffers there stay pageable\n",
                             r.first, r.second, hipGetErrorString(e));
             } else {
+                user_ranges().mark_ready(r.first);
                 g_map_gen.fetch_add(1, std::memory_order_release);
                 regs_.fetch_add(1, std::memory_order_relaxed);
                 reg_us_.fetch_add(dt, std::memory_order_relaxed);
@@ -1829,6 +1883,7 @@ int ecd_host_register(void *p, size_t bytes)
         set_err("hipHostRegister", e);
         return e == hipErrorHostMemoryAlreadyRegistered ? -EEXIST : -ENOMEM;
     }
+    user_ranges().mark_ready(p);
     g_map_gen.fetch_add(1, std::memory_order_release);
     return 0;
 }

@@ -473,12 +473,15 @@ obs_gbps(int eng, int op, uint32_t k, uint64_t user)
 
 /* 1: send this call to the engine the router did not pick, to re-sample it
  * (every 8th such call while the slot has fewer than 4 samples, then every
- * 64th) */
+ * 64th, or every 512th when that engine is estimated at over 4x the time of
+ * the one picked: a cache-resident 1 MiB call codes in ~20 us on the CPU,
+ * and one in 64 of them sent to a GPU 5x slower cost a tight loop of such
+ * calls ~25 %, tools/kbench/xover_cells.sh, profiles/r05/r05ai_xover_*.log) */
 static int
-obs_explore(int eng, int op, uint32_t k, uint64_t user)
+obs_explore(int eng, int op, uint32_t k, uint64_t user, int far)
 {
     ecm_obs_t *o = obs_slot(eng, op, k, user);
-    const uint32_t every = __atomic_load_n(&o->n, __ATOMIC_RELAXED) < 4 ? 8 : 64;
+    const uint32_t every = __atomic_load_n(&o->n, __ATOMIC_RELAXED) < 4 ? 8 : far ? 512 : 64;
 
     if (!ecm_x.adapt || user < ECM_OBS_EXPLORE)
         return 0;
@@ -883,15 +886,24 @@ route_gpu(const ecm_ctx_t *ctx, uint64_t user, uint64_t moved, int op,
     if (ctx->engine == ECM_ENGINE_CPU || ecm_x.always || moved < ecm_x.cpu_below ||
         r == ECM_ROUTE_CPU_BUSY)
         return gpu;
-    if (gpu) {
-        if (obs_explore(ECM_OBS_CPU, op, ctx->k, user))
-            gpu = 0;
-    } else {
-        if (*staged == ECM_STAGED_UNKNOWN && user >= ECM_OBS_EXPLORE)
-            *staged = staged_of(arg);
-        if (*staged != ECM_STAGED_UNKNOWN &&
-            obs_explore(gpu_obs_engine(*staged, moved), op, ctx->k, user))
+    if (user < ECM_OBS_EXPLORE)
+        return gpu;
+    if (*staged == ECM_STAGED_UNKNOWN)
+        *staged = staged_of(arg);
+    {
+        double c, g, lat;
+
+        xover_costs(ctx->k, ctx->isa, user, moved, op, *staged, ecd_host_inflight(), &c, &g,
+                    &lat);
+        if (gpu) {
+            if (obs_explore(ECM_OBS_CPU, op, ctx->k, user, c > 4.0 * g))
+                gpu = 0;
+        } else if (route_cpu(ctx, user, moved, op, *staged) != ECM_ROUTE_CPU_BUSY &&
+                   obs_explore(gpu_obs_engine(*staged, moved), op, ctx->k, user, g > 4.0 * c)) {
+            /* (not while other callers keep the CPU busy and the call's
+             * staging copies would cost more CPU than coding it) */
             gpu = 1;
+        }
     }
     return gpu;
 }
