@@ -539,12 +539,12 @@ int device_numa(int dev)
  * calling thread's first touch, i.e. wherever the caller happens to run --
  * on a 2-socket host half the ranks would stage across the socket link.
  * Node < 0, or any step failing: hipHostMalloc. */
-std::mutex g_numa_mu;
+std::shared_mutex g_numa_mu;        /* shared: the lookups of every host call */
 std::map<void *, size_t> g_numa_allocs;
 
 bool numa_alloc_live(const void *p, size_t n)
 {
-    std::lock_guard<std::mutex> g(g_numa_mu);
+    std::shared_lock<std::shared_mutex> g(g_numa_mu);
     auto it = g_numa_allocs.upper_bound(const_cast<void *>(p));
     if (it == g_numa_allocs.begin())
         return false;
@@ -567,7 +567,7 @@ void *pinned_alloc(size_t bytes, int node)
             memset(p, 0, len);                       /* fault in on the node */
             if (hipHostRegister(p, len, hipHostRegisterMapped) == hipSuccess) {
                 g_map_gen.fetch_add(1, std::memory_order_release);
-                std::lock_guard<std::mutex> g(g_numa_mu);
+                std::unique_lock<std::shared_mutex> g(g_numa_mu);
                 g_numa_allocs[p] = len;
                 return p;
             }
@@ -590,7 +590,7 @@ void pinned_free(void *p)
         return;
     size_t len = 0;
     {
-        std::lock_guard<std::mutex> g(g_numa_mu);
+        std::unique_lock<std::shared_mutex> g(g_numa_mu);
         auto it = g_numa_allocs.find(p);
         if (it != g_numa_allocs.end()) {
             len = it->second;
