@@ -101,6 +101,34 @@ bool nt_staging(uint64_t in_bytes)
     return in_bytes > kNtStagingBytes;
 }
 
+/* A/B only (EC_MI355X_CHUNK_MB, default off): input bytes per launch of a
+ * large single-pattern device call on the non-temporal path.  A 16+4 encode
+ * streams slower per byte as one launch grows (2 GiB 0.815 ms, 8 GiB 3.53),
+ * and 1 GiB launches take back a third of that, but every other call loses
+ * the launch boundaries.  After 150 ms of load, 20 launches, medians of
+ * three rounds, ms per call, one launch / 512 MiB / 1 GiB launches
+ * (profiles/r05/r05an_sizes.log, r05ao_chunkab.log, r05ap_chunkab.log):
+ *   16+4 encode 8 GiB  3.485 / 3.412 / 3.399
+ *   16+4 encode 2 GiB  0.822 / 0.825 / 0.819
+ *   4+2 decode 2 GiB   0.662 / 0.678 / 0.676
+ *   8+4 encode 2 GiB   0.893 / 0.904 / 0.905 */
+uint64_t launch_chunk_bytes()
+{
+    static const uint64_t v = [] {
+        const char *e = getenv("EC_MI355X_CHUNK_MB");
+        return e ? strtoull(e, nullptr, 10) << 20 : 0ull;
+    }();
+    return v;
+}
+
+/* Stripes per launch for stripes of `stripe_bytes` input: a multiple of 8
+ * (every tile kernel's tile divides it), 0 = the whole call. */
+uint64_t chunk_stripes(uint64_t nstripes, uint64_t stripe_bytes)
+{
+    const uint64_t c = launch_chunk_bytes() / stripe_bytes / 8 * 8;
+    return c && c < nstripes ? c : 0;
+}
+
 /* hipFuncAttributeMaxDynamicSharedMemorySize is per device: set it once per
  * (kernel, device), for the device current on the launching thread (a
  * process-wide once-flag left every GPU but the first unconfigured). */
@@ -258,8 +286,21 @@ int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSr
 {
     const bool aligned = ((uintptr_t)src.in & 15u) == 0;
     if constexpr (SM == 0)
-        if (aligned && nt_staging(nstripes * k * ECD_CHUNK))
-            return encode_tiles_la<SM, kLdsDmaNT>(s, k, n, nstripes, src, out);
+        if (aligned && nt_staging(nstripes * k * ECD_CHUNK)) {
+            const uint64_t cs = chunk_stripes(nstripes, (uint64_t)k * ECD_CHUNK);
+            if (!cs)
+                return encode_tiles_la<SM, kLdsDmaNT>(s, k, n, nstripes, src, out);
+            void *o[ECD_MAX_ROWS];
+            for (uint64_t t0 = 0; t0 < nstripes; t0 += cs) {
+                const uint64_t m = nstripes - t0 < cs ? nstripes - t0 : cs;
+                for (uint32_t i = 0; i < n; ++i)
+                    o[i] = static_cast<uint8_t *>(out[i]) + t0 * ECD_CHUNK;
+                const EncSrc c{src.in + t0 * k * ECD_CHUNK, nullptr};
+                if (int rc = encode_tiles_la<SM, kLdsDmaNT>(s, k, n, m, c, o))
+                    return rc;
+            }
+            return 0;
+        }
     /* a byte-misaligned input (a partial write's interior, or a device
      * buffer at an odd offset): dword-aligned loads shifted through
      * registers (SM = 3, ec_kernels_impl.h stage_tile_shift) instead of
@@ -772,12 +813,29 @@ int combine_any(hipStream_t s, const ecd_combine_desc_t *d)
     /* staging policy by the call's input bytes; the host-buffer fallback
      * (NTS = false: pinned memory over PCIe) keeps the default policy */
     if (rc == 0) {
-        if constexpr (NTS)
-            rc = nt_staging(a.nstripes * a.k * ECD_CHUNK) && inputs_aligned(a)
-                     ? launch_combine_k<NTS, kLdsDmaNT>(s, a)
-                     : launch_combine_k<NTS, kLdsDmaDefault>(s, a);
-        else
+        if constexpr (NTS) {
+            const bool nt = nt_staging(a.nstripes * a.k * ECD_CHUNK) && inputs_aligned(a);
+            const uint64_t cs = nt && !a.group_pattern
+                                    ? chunk_stripes(a.nstripes, (uint64_t)a.k * ECD_CHUNK) : 0;
+            if (cs) {
+                for (uint64_t t0 = 0; t0 < a.nstripes && rc == 0; t0 += cs) {
+                    CombineArgs c = a;
+                    c.nstripes = a.nstripes - t0 < cs ? a.nstripes - t0 : cs;
+                    for (u32 p = 0; p < ECD_MAX_ROWS; ++p) {
+                        if (c.in_base[p])
+                            c.in_base[p] += t0 * a.in_stride;
+                        if (c.out_base[p])
+                            c.out_base[p] += t0 * a.out_stride;
+                    }
+                    rc = launch_combine_k<NTS, kLdsDmaNT>(s, c);
+                }
+            } else {
+                rc = nt ? launch_combine_k<NTS, kLdsDmaNT>(s, a)
+                        : launch_combine_k<NTS, kLdsDmaDefault>(s, a);
+            }
+        } else {
             rc = launch_combine_k<NTS, kLdsDmaDefault>(s, a);
+        }
     }
     if (ref.slot >= 0)
         (void)pat_tables().release(ref, s);   /* a failure drained s: the call stands */

@@ -10,7 +10,10 @@ EC_MI355X_ZCDB=0 runs host-buffer combines (k <= 8) through the one tile per
 block zero-copy kernel instead of the persistent double-buffered one (the
 default since r04; =1 forces it), each with host encode, decode, heal and
 mixed calls; EC_ZC_TPB (fixed tiles per block) and EC_ZC_INFLIGHT_KB (input
-bytes in flight per round of tiles) size the persistent zero-copy grid.
+bytes in flight per round of tiles) size the persistent zero-copy grid;
+EC_MI355X_CHUNK_MB=1 (with LDSNT=1; an A/B knob, off by default) cuts every
+single-pattern device call into launches of 1 MiB of input, ragged last
+launch included.
 Each runs here in its own process through the C ABI, bit-exact against the
 oracle on device-resident encode, full / partial decode (ragged tiles
 included) and mixed decode.
@@ -114,13 +117,17 @@ print("ok")
 
 KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1"),
          ("EC_MI355X_ZCDB", "0"), ("EC_MI355X_ZCDB", "1"), ("EC_ZC_TPB", "1"), ("EC_ZC_TPB", "16"),
-         ("EC_ZC_INFLIGHT_KB", "64")]
+         ("EC_ZC_INFLIGHT_KB", "64"), ("EC_MI355X_CHUNK_MB", "1")]
 
 
 @pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])
 def test_ab_instantiation_bit_exact(knob, value):
     env = dict(os.environ, EC_MI355X_QUIET="1", EC_GPU_ALWAYS="1")
     env[knob] = value
+    if knob == "EC_MI355X_CHUNK_MB":
+        # launches of 1 MiB of input (128-512 stripes): chunking engages on
+        # the non-temporal path only, which these small calls take when forced
+        env["EC_MI355X_LDSNT"] = "1"
     r = subprocess.run([sys.executable, "-c", SCRIPT], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=170)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]

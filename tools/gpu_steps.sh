@@ -49,6 +49,7 @@ for step in "$@"; do
     ablib) run ablib 900 bash tools/ab_lib.sh "${AB_ARGS:-mixed:8+4 1 mixed:16+4:64 1 dec:8+4:FF0 1}" ;;
     hsweep3) run hsweep3 400 bash -c 'for m in auto gpu cpu; do echo "== $m"; if [ $m = gpu ]; then E=1; else E=0; fi; EC_GPU_ALWAYS=$E python3 bench.py --heal-sweep $m --steps 256 || exit 1; done' ;;
     kb3) run kb3 600 tools/kbench/kb3 ${KB3_ARGS:-1 7 all} ;;
+    sizes) run sizes 900 bash -c 'for r in 1 2; do for c in ${SIZE_CASES:-"enc:16+4 2" "enc:16+4 8" "dec:4+2:3C 1" "dec:4+2:3C 4" "enc:4+2 1" "enc:4+2 4"}; do set -- $c; echo "== round $r $1 $2 GiB"; python3 bench.py --only $1 --gib $2 --steps 20 --warmup 5 --warm-ms 150 || exit 1; done; done' ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
