@@ -155,7 +155,15 @@ class Ctx:
         user = nst * CHUNK * k
         w0 = self.rank * user // 8 if word0 is None else word0
         data = synth.fill_device(torch, user, self.dev, word0=w0)
-        frags = [torch.empty(nst * CHUNK, dtype=torch.uint8, device=self.dev) for _ in range(n)]
+        stagger = int(os.environ.get("EC_BENCH_FRAG_STAGGER", "0"))   # A/B: placement
+        if stagger:
+            # the n fragments as views of one allocation, bases `stagger`
+            # bytes off a multiple of the fragment size
+            span = nst * CHUNK + stagger
+            blob = torch.empty(span * n, dtype=torch.uint8, device=self.dev)
+            frags = [blob[i * span:i * span + nst * CHUNK] for i in range(n)]
+        else:
+            frags = [torch.empty(nst * CHUNK, dtype=torch.uint8, device=self.dev) for _ in range(n)]
         L = self.g.ECMatrixList(k, n)
         L.encode_device(self.dev.index, self.sp, nst, data, frags)
         fx = fixture(case, self.rank) if case else None

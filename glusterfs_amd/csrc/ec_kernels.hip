@@ -101,6 +101,33 @@ bool nt_staging(uint64_t in_bytes)
     return in_bytes > kNtStagingBytes;
 }
 
+/* A/B only: EC_MI355X_TILE_PERM=1 walks the tile encoders' tiles in
+ * golden-ratio order, so the tiles in flight at once are spread over the
+ * whole call instead of one contiguous window of every fragment; =2 gives
+ * each XCD its own contiguous run of tiles. */
+uint32_t tile_perm(uint64_t tiles)
+{
+    static const int mode = [] {
+        const char *e = getenv("EC_MI355X_TILE_PERM");
+        return e ? atoi(e) : 0;
+    }();
+    if (mode == 0 || tiles < 2 || tiles > 0xFFFFFFFFull)
+        return 0;
+    if (mode == 2)
+        return 0xFFFFFFFFu;             /* XCD-contiguous (ec_kernels_impl.h enc_tile) */
+    uint64_t p = (uint64_t)((double)tiles * 0.6180339887498949) | 1u;
+    for (;; p += 2) {
+        uint64_t a = p % tiles, b = tiles;
+        while (a) {
+            const uint64_t t = b % a;
+            b = a;
+            a = t;
+        }
+        if (b == 1)
+            return (uint32_t)(p % tiles);
+    }
+}
+
 /* A/B only (EC_MI355X_CHUNK_MB, default off): input bytes per launch of a
  * large single-pattern device call on the non-temporal path.  A 16+4 encode
  * streams slower per byte as one launch grows (2 GiB 0.815 ms, 8 GiB 3.53),
@@ -285,6 +312,8 @@ int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSr
                  void *const *out)
 {
     const bool aligned = ((uintptr_t)src.in & 15u) == 0;
+    if constexpr (SM == 0)
+        src.perm = tile_perm((nstripes + 3) / 4);
     if constexpr (SM == 0)
         if (aligned && nt_staging(nstripes * k * ECD_CHUNK)) {
             const uint64_t cs = chunk_stripes(nstripes, (uint64_t)k * ECD_CHUNK);

@@ -454,7 +454,25 @@ __device__ __forceinline__ void wave_lds_sync()
 struct EncSrc {
     const uint8_t *in;
     const uint8_t *edge;
+    /* tile order (A/B, EC_MI355X_TILE_PERM): block b codes tile
+     * b * perm mod gridDim.x (perm coprime with the grid), 0 = tile b,
+     * 0xFFFFFFFF = each XCD its own contiguous run of tiles */
+    uint32_t perm = 0;
 };
+
+/* the tile of this block under src.perm (a bijection on [0, gridDim.x)) */
+__device__ __forceinline__ uint64_t enc_tile(const EncSrc &src)
+{
+    if (src.perm == 0)
+        return blockIdx.x;
+    if (src.perm == 0xFFFFFFFFu) {
+        /* XCD-contiguous: blocks go round-robin to the 8 XCDs, so XCD x
+         * (blocks b = x mod 8) walks its own contiguous eighth of the tiles */
+        const uint64_t g = gridDim.x, q = g / 8, r = g % 8, x = blockIdx.x % 8;
+        return x * q + (x < r ? x : r) + blockIdx.x / 8;
+    }
+    return (uint64_t)blockIdx.x * src.perm % gridDim.x;
+}
 
 /* RA staging: the same plane-major tile as stage_tile, through registers --
  * piece i (16 B) = ((p * 8 + b) * T + s) * 4 + q is 16 bytes at
@@ -691,7 +709,7 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const EncSrc src, co
     constexpr u32 LPS = 16 / CW;               /* lanes per stripe */
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
-    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const uint64_t t0 = enc_tile(src) * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
     stage_encode_tile<K, T, NW, SM, LA>(lds, src, t0, nstripes, wave, lane);
@@ -780,7 +798,7 @@ __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
     constexpr u32 SUB = T / 4, NW = (N / RB) * SUB;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
-    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const uint64_t t0 = enc_tile(src) * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
     stage_encode_tile<K, T, NW, SM, LA>(lds, src, t0, nstripes, wave, lane);

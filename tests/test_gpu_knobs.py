@@ -13,7 +13,8 @@ mixed calls; EC_ZC_TPB (fixed tiles per block) and EC_ZC_INFLIGHT_KB (input
 bytes in flight per round of tiles) size the persistent zero-copy grid;
 EC_MI355X_CHUNK_MB=1 (with LDSNT=1; an A/B knob, off by default) cuts every
 single-pattern device call into launches of 1 MiB of input, ragged last
-launch included.
+launch included; EC_MI355X_TILE_PERM=1 / 2 (A/B, off by default) walk the
+tile encoders' tiles in golden-ratio order / as one contiguous run per XCD.
 Each runs here in its own process through the C ABI, bit-exact against the
 oracle on device-resident encode, full / partial decode (ragged tiles
 included) and mixed decode.
@@ -117,7 +118,8 @@ print("ok")
 
 KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1"),
          ("EC_MI355X_ZCDB", "0"), ("EC_MI355X_ZCDB", "1"), ("EC_ZC_TPB", "1"), ("EC_ZC_TPB", "16"),
-         ("EC_ZC_INFLIGHT_KB", "64"), ("EC_MI355X_CHUNK_MB", "1")]
+         ("EC_ZC_INFLIGHT_KB", "64"), ("EC_MI355X_CHUNK_MB", "1"),
+         ("EC_MI355X_TILE_PERM", "1"), ("EC_MI355X_TILE_PERM", "2")]
 
 
 @pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])
