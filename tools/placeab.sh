@@ -6,7 +6,8 @@ mkdir -p gpurun_out
 TAG=${TAG:-r05ar}
 {
 for r in 1 2 3; do
- for c in ${PLACE_CASES:-"enc:16+4 8" "enc:16+4 2" "dec:4+2:3C 1" "enc:4+2 1"}; do
+ IFS=, read -ra CASES <<< "${PLACE_CASES:-enc:16+4 8,enc:16+4 2,dec:4+2:3C 1,enc:4+2 1}"
+ for c in "${CASES[@]}"; do
   set -- $c
   for st in ${STAGGERS:-0 256 4096 2162688}; do
    echo "== round $r $1 $2 GiB stagger $st"
