@@ -101,18 +101,34 @@ bool nt_staging(uint64_t in_bytes)
     return in_bytes > kNtStagingBytes;
 }
 
-/* A/B only: EC_MI355X_TILE_PERM=1 walks the tile encoders' tiles in
- * golden-ratio order, so the tiles in flight at once are spread over the
- * whole call instead of one contiguous window of every fragment; =2 gives
- * each XCD its own contiguous run of tiles. */
-uint32_t tile_perm(uint64_t tiles)
+/* Tile order of the tile encoders.  Shipped: block b codes tile b, except
+ * for 16+4 encodes of >= 4 GiB of input, where each XCD walks its own
+ * contiguous run of tiles (blocks go round-robin to the 8 XCDs; ec_kernels_
+ * impl.h enc_tile).  A 16+4 encode depends on where its 20 fragments sit
+ * (up to +-12 %); at 4-8 GiB the XCD runs were faster for
+ * seven placements of eight (4 % on average, the worst placement 7 %), at
+ * 2 GiB slower for five of six (3 % on average).  Medians of three
+ * rounds after 150 ms of load, ms per call, tile b / XCD runs
+ * (profiles/r05/r05at_permab.log, r05au_permab.log, r05av_permab.log):
+ *   8 GiB, 6 placements  3.194-3.559 / 3.170-3.296 (mean 3.352 / 3.208)
+ *   4 GiB, 2 placements  1.667, 1.604 / 1.627, 1.585
+ *   2 GiB, 6 placements  0.801-0.913 / 0.812-0.944 (mean 0.834 / 0.859)
+ * For 4+2 and 8+4 at 8 GiB the sign depends on the placement (+-7 %), so
+ * they keep tile b.  EC_MI355X_TILE_PERM (A/B): 0 = tile b always, 1 =
+ * golden-ratio order (the tiles in flight spread over the call: 20-28 %
+ * slower everywhere, r05as), 2 = XCD runs always. */
+constexpr uint64_t kXcdTilesBytes = 4ull << 30;
+
+uint32_t tile_perm(uint64_t tiles, uint32_t k)
 {
     static const int mode = [] {
         const char *e = getenv("EC_MI355X_TILE_PERM");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : -1;
     }();
-    if (mode == 0 || tiles < 2 || tiles > 0xFFFFFFFFull)
+    if (tiles < 2 || tiles > 0xFFFFFFFFull || mode == 0)
         return 0;
+    if (mode < 0)                       /* unset: the shipped rule */
+        return k == 16 && tiles * 4 * k * ECD_CHUNK >= kXcdTilesBytes ? 0xFFFFFFFFu : 0;
     if (mode == 2)
         return 0xFFFFFFFFu;             /* XCD-contiguous (ec_kernels_impl.h enc_tile) */
     uint64_t p = (uint64_t)((double)tiles * 0.6180339887498949) | 1u;
@@ -313,7 +329,7 @@ int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSr
 {
     const bool aligned = ((uintptr_t)src.in & 15u) == 0;
     if constexpr (SM == 0)
-        src.perm = tile_perm((nstripes + 3) / 4);
+        src.perm = tile_perm((nstripes + 3) / 4, k);
     if constexpr (SM == 0)
         if (aligned && nt_staging(nstripes * k * ECD_CHUNK)) {
             const uint64_t cs = chunk_stripes(nstripes, (uint64_t)k * ECD_CHUNK);
