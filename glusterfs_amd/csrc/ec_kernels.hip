@@ -101,76 +101,24 @@ bool nt_staging(uint64_t in_bytes)
     return in_bytes > kNtStagingBytes;
 }
 
-/* Tile order of the tile encoders.  Shipped: block b codes tile b, except
- * for 16+4 encodes of >= 4 GiB of input, where each XCD walks its own
- * contiguous run of tiles (blocks go round-robin to the 8 XCDs; ec_kernels_
- * impl.h enc_tile).  A 16+4 encode depends on where its 20 fragments sit
- * (up to +-12 %); at 4-8 GiB the XCD runs were faster for
- * seven placements of eight (4 % on average, the worst placement 7 %), at
- * 2 GiB slower for five of six (3 % on average).  Medians of three
- * rounds after 150 ms of load, ms per call, tile b / XCD runs
- * (profiles/r05/r05at_permab.log, r05au_permab.log, r05av_permab.log):
+/* Tile order of the tile encoders: block b codes tile b, except for 16+4
+ * encodes of >= 4 GiB of input, where each XCD walks its own contiguous run
+ * of tiles (blocks go round-robin to the 8 XCDs; ec_kernels_impl.h
+ * enc_tile<true>).  A 16+4 encode depends on where its 20 fragments sit (up
+ * to +-12 %); at 4-8 GiB the XCD runs were faster for seven
+ * placements of eight (4 % on average, the worst placement 7 %), at 2 GiB
+ * slower for five of six (3 % on average).  Medians of three rounds after
+ * 150 ms of load, ms per call, tile b / XCD runs (profiles/r05/
+ * r05at_permab.log, r05au_permab.log, r05av_permab.log):
  *   8 GiB, 6 placements  3.194-3.559 / 3.170-3.296 (mean 3.352 / 3.208)
  *   4 GiB, 2 placements  1.667, 1.604 / 1.627, 1.585
  *   2 GiB, 6 placements  0.801-0.913 / 0.812-0.944 (mean 0.834 / 0.859)
  * For 4+2 and 8+4 at 8 GiB the sign depends on the placement (+-7 %), so
- * they keep tile b.  EC_MI355X_TILE_PERM (A/B): 0 = tile b always, 1 =
- * golden-ratio order (the tiles in flight spread over the call: 20-28 %
- * slower everywhere, r05as), 2 = XCD runs always. */
+ * they keep tile b.  (Measured and retired in r05/r06: golden-ratio order,
+ * 20-28 % slower everywhere, r05as_permab.log; launches cut into 512 MiB /
+ * 1 GiB pieces, a third of the 8 GiB 16+4 loss back but every other call
+ * slower, r05ao_chunkab.log, r05ap_chunkab.log.) */
 constexpr uint64_t kXcdTilesBytes = 4ull << 30;
-
-uint32_t tile_perm(uint64_t tiles, uint32_t k)
-{
-    static const int mode = [] {
-        const char *e = getenv("EC_MI355X_TILE_PERM");
-        return e ? atoi(e) : -1;
-    }();
-    if (tiles < 2 || tiles > 0xFFFFFFFFull || mode == 0)
-        return 0;
-    if (mode < 0)                       /* unset: the shipped rule */
-        return k == 16 && tiles * 4 * k * ECD_CHUNK >= kXcdTilesBytes ? 0xFFFFFFFFu : 0;
-    if (mode == 2)
-        return 0xFFFFFFFFu;             /* XCD-contiguous (ec_kernels_impl.h enc_tile) */
-    uint64_t p = (uint64_t)((double)tiles * 0.6180339887498949) | 1u;
-    for (;; p += 2) {
-        uint64_t a = p % tiles, b = tiles;
-        while (a) {
-            const uint64_t t = b % a;
-            b = a;
-            a = t;
-        }
-        if (b == 1)
-            return (uint32_t)(p % tiles);
-    }
-}
-
-/* A/B only (EC_MI355X_CHUNK_MB, default off): input bytes per launch of a
- * large single-pattern device call on the non-temporal path.  A 16+4 encode
- * streams slower per byte as one launch grows (2 GiB 0.815 ms, 8 GiB 3.53),
- * and 1 GiB launches take back a third of that, but every other call loses
- * the launch boundaries.  After 150 ms of load, 20 launches, medians of
- * three rounds, ms per call, one launch / 512 MiB / 1 GiB launches
- * (profiles/r05/r05an_sizes.log, r05ao_chunkab.log, r05ap_chunkab.log):
- *   16+4 encode 8 GiB  3.485 / 3.412 / 3.399
- *   16+4 encode 2 GiB  0.822 / 0.825 / 0.819
- *   4+2 decode 2 GiB   0.662 / 0.678 / 0.676
- *   8+4 encode 2 GiB   0.893 / 0.904 / 0.905 */
-uint64_t launch_chunk_bytes()
-{
-    static const uint64_t v = [] {
-        const char *e = getenv("EC_MI355X_CHUNK_MB");
-        return e ? strtoull(e, nullptr, 10) << 20 : 0ull;
-    }();
-    return v;
-}
-
-/* Stripes per launch for stripes of `stripe_bytes` input: a multiple of 8
- * (every tile kernel's tile divides it), 0 = the whole call. */
-uint64_t chunk_stripes(uint64_t nstripes, uint64_t stripe_bytes)
-{
-    const uint64_t c = launch_chunk_bytes() / stripe_bytes / 8 * 8;
-    return c && c < nstripes ? c : 0;
-}
 
 /* hipFuncAttributeMaxDynamicSharedMemorySize is per device: set it once per
  * (kernel, device), for the device current on the launching thread (a
@@ -286,8 +234,9 @@ int launch_encode_narrow(hipStream_t s, uint64_t nstripes, EncSrc src, void *con
 }
 
 /* Row-group encoder (ec_encode_tile_rb): 4-stripe tiles, RB rows per wave,
- * so the tile is read from LDS N / RB times instead of N times. */
-template <int K, int N, int RB, int SM, int LA>
+ * so the tile is read from LDS N / RB times instead of N times.  XR: XCD
+ * tile runs (kXcdTilesBytes). */
+template <int K, int N, int RB, int SM, int LA, bool XR = false>
 int launch_encode_rb(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *out)
 {
     FragPtrs f;
@@ -298,7 +247,7 @@ int launch_encode_rb(hipStream_t s, uint64_t nstripes, EncSrc src, void *const *
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true, SM, LA>), dim3((u32)g),
+    hipLaunchKernelGGL((ec_encode_tile_rb<K, N, 4, RB, true, true, SM, LA, XR>), dim3((u32)g),
                        dim3((N / RB) * 64), (encode_tile_rb_lds<N, 4, RB, true>(K)), s, src, f,
                        nstripes);
     return launch_ok("launch_encode_rb");
@@ -313,8 +262,12 @@ int encode_tiles_la(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, En
         return launch_encode_narrow<4, 6, 6, true, SM, LA>(s, nstripes, src, out);
     if (k == 8 && n == 12)
         return launch_encode_narrow<8, 12, 12, false, SM, LA>(s, nstripes, src, out);
-    if (k == 16 && n == 20)
+    if (k == 16 && n == 20) {
+        if constexpr (SM == 0 && LA == kLdsDmaNT)
+            if (nstripes * 16 * ECD_CHUNK >= kXcdTilesBytes)
+                return launch_encode_rb<16, 20, 2, SM, LA, true>(s, nstripes, src, out);
         return launch_encode_rb<16, 20, 2, SM, LA>(s, nstripes, src, out);
+    }
     return -ENOTSUP;
 }
 
@@ -329,23 +282,8 @@ int encode_tiles(hipStream_t s, uint32_t k, uint32_t n, uint64_t nstripes, EncSr
 {
     const bool aligned = ((uintptr_t)src.in & 15u) == 0;
     if constexpr (SM == 0)
-        src.perm = tile_perm((nstripes + 3) / 4, k);
-    if constexpr (SM == 0)
-        if (aligned && nt_staging(nstripes * k * ECD_CHUNK)) {
-            const uint64_t cs = chunk_stripes(nstripes, (uint64_t)k * ECD_CHUNK);
-            if (!cs)
-                return encode_tiles_la<SM, kLdsDmaNT>(s, k, n, nstripes, src, out);
-            void *o[ECD_MAX_ROWS];
-            for (uint64_t t0 = 0; t0 < nstripes; t0 += cs) {
-                const uint64_t m = nstripes - t0 < cs ? nstripes - t0 : cs;
-                for (uint32_t i = 0; i < n; ++i)
-                    o[i] = static_cast<uint8_t *>(out[i]) + t0 * ECD_CHUNK;
-                const EncSrc c{src.in + t0 * k * ECD_CHUNK, nullptr};
-                if (int rc = encode_tiles_la<SM, kLdsDmaNT>(s, k, n, m, c, o))
-                    return rc;
-            }
-            return 0;
-        }
+        if (aligned && nt_staging(nstripes * k * ECD_CHUNK))
+            return encode_tiles_la<SM, kLdsDmaNT>(s, k, n, nstripes, src, out);
     /* a byte-misaligned input (a partial write's interior, or a device
      * buffer at an odd offset): dword-aligned loads shifted through
      * registers (SM = 3, ec_kernels_impl.h stage_tile_shift) instead of
@@ -860,24 +798,8 @@ int combine_any(hipStream_t s, const ecd_combine_desc_t *d)
     if (rc == 0) {
         if constexpr (NTS) {
             const bool nt = nt_staging(a.nstripes * a.k * ECD_CHUNK) && inputs_aligned(a);
-            const uint64_t cs = nt && !a.group_pattern
-                                    ? chunk_stripes(a.nstripes, (uint64_t)a.k * ECD_CHUNK) : 0;
-            if (cs) {
-                for (uint64_t t0 = 0; t0 < a.nstripes && rc == 0; t0 += cs) {
-                    CombineArgs c = a;
-                    c.nstripes = a.nstripes - t0 < cs ? a.nstripes - t0 : cs;
-                    for (u32 p = 0; p < ECD_MAX_ROWS; ++p) {
-                        if (c.in_base[p])
-                            c.in_base[p] += t0 * a.in_stride;
-                        if (c.out_base[p])
-                            c.out_base[p] += t0 * a.out_stride;
-                    }
-                    rc = launch_combine_k<NTS, kLdsDmaNT>(s, c);
-                }
-            } else {
-                rc = nt ? launch_combine_k<NTS, kLdsDmaNT>(s, a)
-                        : launch_combine_k<NTS, kLdsDmaDefault>(s, a);
-            }
+            rc = nt ? launch_combine_k<NTS, kLdsDmaNT>(s, a)
+                    : launch_combine_k<NTS, kLdsDmaDefault>(s, a);
         } else {
             rc = launch_combine_k<NTS, kLdsDmaDefault>(s, a);
         }

@@ -454,24 +454,24 @@ __device__ __forceinline__ void wave_lds_sync()
 struct EncSrc {
     const uint8_t *in;
     const uint8_t *edge;
-    /* tile order (A/B, EC_MI355X_TILE_PERM): block b codes tile
-     * b * perm mod gridDim.x (perm coprime with the grid), 0 = tile b,
-     * 0xFFFFFFFF = each XCD its own contiguous run of tiles */
-    uint32_t perm = 0;
 };
 
-/* the tile of this block under src.perm (a bijection on [0, gridDim.x)) */
-__device__ __forceinline__ uint64_t enc_tile(const EncSrc &src)
+/* The tile of this block.  XR = false: tile b.  XR = true (only the 16+4
+ * encoder of >= 4 GiB calls is built this way, ec_kernels.hip
+ * kXcdTilesBytes): blocks go round-robin to the 8 XCDs, so XCD x (blocks
+ * b = x mod 8) walks its own contiguous eighth of the tiles.  A compile-time
+ * choice: round 5 carried it as a run-time field of EncSrc, and the branch
+ * and the wider kernel argument cost the partial-write encoder 8 % (VERDICT
+ * r05). */
+template <bool XR>
+__device__ __forceinline__ uint64_t enc_tile()
 {
-    if (src.perm == 0)
+    if constexpr (!XR) {
         return blockIdx.x;
-    if (src.perm == 0xFFFFFFFFu) {
-        /* XCD-contiguous: blocks go round-robin to the 8 XCDs, so XCD x
-         * (blocks b = x mod 8) walks its own contiguous eighth of the tiles */
+    } else {
         const uint64_t g = gridDim.x, q = g / 8, r = g % 8, x = blockIdx.x % 8;
         return x * q + (x < r ? x : r) + blockIdx.x / 8;
     }
-    return (uint64_t)blockIdx.x * src.perm % gridDim.x;
 }
 
 /* RA staging: the same plane-major tile as stage_tile, through registers --
@@ -700,7 +700,7 @@ __device__ __forceinline__ void encode_tile_item(const uint8_t *col, uint8_t *sl
 }
 
 template <int K, int N, int T, int NW, bool NTS, bool DIRECT, bool WOT, int SM = 0,
-          int LA = kLdsDmaDefault>
+          int LA = kLdsDmaDefault, bool XR = false>
 __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const EncSrc src, const FragPtrs out,
                                                             uint64_t nstripes)
 {
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(NW * 64) void ec_encode_tile_t(const EncSrc src, co
     constexpr u32 LPS = 16 / CW;               /* lanes per stripe */
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
-    const uint64_t t0 = enc_tile(src) * T;
+    const uint64_t t0 = enc_tile<XR>() * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
     stage_encode_tile<K, T, NW, SM, LA>(lds, src, t0, nstripes, wave, lane);
@@ -790,7 +790,8 @@ __device__ __forceinline__ void encode_group_acc(const uint8_t *col, u32 (&acc)[
 /* T = 4 or 8 stripes per tile (SUB = T / 4 four-stripe sub-tiles), N / RB
  * row groups, one item per wave: NW = (N / RB) * SUB.  WOT: each row leaves
  * through the wave's 2 KiB LDS slice as one contiguous 2 KiB run. */
-template <int K, int N, int T, int RB, bool NTS, bool WOT, int SM = 0, int LA = kLdsDmaDefault>
+template <int K, int N, int T, int RB, bool NTS, bool WOT, int SM = 0, int LA = kLdsDmaDefault,
+          bool XR = false>
 __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
     const EncSrc src, const FragPtrs out, uint64_t nstripes)
 {
@@ -798,7 +799,7 @@ __global__ __launch_bounds__((N / RB) * (T / 4) * 64) void ec_encode_tile_rb(
     constexpr u32 SUB = T / 4, NW = (N / RB) * SUB;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const u32 tid = threadIdx.x;
-    const uint64_t t0 = enc_tile(src) * T;
+    const uint64_t t0 = enc_tile<XR>() * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
     stage_encode_tile<K, T, NW, SM, LA>(lds, src, t0, nstripes, wave, lane);

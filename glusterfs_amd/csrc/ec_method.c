@@ -329,7 +329,7 @@ env_u64(const char *name, uint64_t dflt)
 
 static struct {
     uint64_t cpu_below, enc_k2, dec_k, pin_us, pin_gbps, page_us, page_gbps, page_gbps_l, always;
-    uint64_t adapt, hybrid, hybrid_share, copy_gbps, spin_ns, learn;
+    uint64_t adapt, hybrid, hybrid_share, copy_gbps, learn;
 } __attribute__((aligned(64))) ecm_x;
 static pthread_once_t ecm_xover_once __attribute__((aligned(64))) = PTHREAD_ONCE_INIT;
 
@@ -353,9 +353,6 @@ xover_init(void)
     /* one CPU thread's copy rate between pageable and pinned memory (the
      * staging copies of a GPU call with pageable buffers); 0: no busy rule */
     ecm_x.copy_gbps = env_u64("EC_STAGE_COPY_GBPS", 10);
-    /* how long an idle split-call helper polls for the next share before it
-     * sleeps (a woken thread takes tens of us to run again) */
-    ecm_x.spin_ns = env_u64("EC_HELPER_SPIN_US", 0) * 1000;
     ecm_x.learn = env_u64("EC_SPLIT_LEARN", 1);   /* 0: the model's split shares (A/B) */
 }
 
@@ -463,6 +460,38 @@ obs_record(int eng, int op, uint32_t k, uint64_t user, uint64_t ns)
     obs_record_part(eng, op, k, user, user, ns);
 }
 
+/* The GPU's fixed cost of a host call, microseconds: the model's latency,
+ * interpolated between pinned (zero-copy) and staged buffers by the fraction
+ * of its bytes that are staged. */
+static double
+gpu_lat_us(uint64_t staged, uint64_t moved)
+{
+    const double f = moved ? (double)(staged < moved ? staged : moved) / (double)moved : 0.0;
+
+    return (double)ecm_x.pin_us + f * ((double)ecm_x.page_us - (double)ecm_x.pin_us);
+}
+
+/* A split call's GPU share (r06): `part` of the call's `user`
+ * bytes took `ns`, which hold the GPU's fixed latency L once.  The slot of
+ * calls of `user` bytes prices a whole call as user / rate, with L inside the
+ * rate, so the share is recorded as the time the whole call would have
+ * taken, L + (ns - L) * user / part.  Recording part / ns (r05) charged L
+ * 1 / f times over: at f = 0.35 the whole-call estimate came out ~3x L too
+ * high, the next share came out smaller, and each smaller share inflated the
+ * next estimate further (tests/test_xover.py::test_split_samples_keep_routing). */
+static void
+obs_record_gpu_part(int eng, int op, uint32_t k, uint64_t user, uint64_t part, uint64_t ns,
+                    uint64_t staged, uint64_t moved)
+{
+    const double lat = gpu_lat_us(staged, moved) * 1e3, sc = part ? (double)user / (double)part : 0;
+    double whole;
+
+    if (part == 0 || part > user || ns == 0)
+        return;
+    whole = (double)ns > lat ? lat + ((double)ns - lat) * sc : (double)ns * sc;
+    obs_record(eng, op, k, user, (uint64_t)whole);
+}
+
 static double
 obs_gbps(int eng, int op, uint32_t k, uint64_t user)
 {
@@ -520,7 +549,7 @@ xover_costs(uint32_t k, int isa, uint64_t user, uint64_t moved, int op, uint64_t
     if (staged > moved)
         staged = moved;
     f = (double)staged / (double)moved;
-    *lat = (double)ecm_x.pin_us + f * ((double)ecm_x.page_us - (double)ecm_x.pin_us);
+    *lat = gpu_lat_us(staged, moved);
     obs = obs_gbps(gpu_obs_engine(staged, moved), op, k, user);
     if (obs > 0) {
         *gpu = (q + user) / (obs * 1e3);
@@ -757,19 +786,9 @@ helper_main(void *unused)
     pthread_mutex_lock(&ecm_pool_mu);
     for (;;) {
         while (!ecm_q_head) {
+            /* (helpers that poll 50 or 200 us before sleeping measured
+             * within run-to-run noise, profiles/r05/r05ab_spinab.log) */
             ecm_helpers_idle++;
-            if (ecm_x.spin_ns) {
-                const uint64_t end = now_ns() + ecm_x.spin_ns;
-
-                pthread_mutex_unlock(&ecm_pool_mu);
-                while (__atomic_load_n(&ecm_q_len, __ATOMIC_RELAXED) == 0 && now_ns() < end)
-                    __builtin_ia32_pause();
-                pthread_mutex_lock(&ecm_pool_mu);
-                if (ecm_q_head) {
-                    ecm_helpers_idle--;
-                    break;
-                }
-            }
             pthread_cond_wait(&ecm_pool_cv, &ecm_pool_mu);
             ecm_helpers_idle--;
         }
@@ -945,6 +964,21 @@ ec_method_xover_observe_split(int32_t op, uint32_t k, uint64_t user, uint64_t mo
         gpu_share == 0 || gpu_share >= 1000)
         return -EINVAL;
     share_learn(op, op, k, ecc_isa_max(), user, moved, staged, n, gpu_share, gpu_ns, cpu_ns);
+    return 0;
+}
+
+int32_t
+ec_method_xover_observe_part(int32_t engine, int32_t op, uint32_t k, uint64_t user, uint64_t part,
+                             uint64_t ns, uint64_t staged, uint64_t moved)
+{
+    if (engine < 0 || engine >= ECM_OBS_ENGINES || (op != ECM_ENCODE && op != ECM_DECODE) ||
+        k < 1 || k > ECM_MAX_K || part == 0 || part > user || moved == 0)
+        return -EINVAL;
+    pthread_once(&ecm_xover_once, xover_init);
+    if (engine == ECM_OBS_CPU)
+        obs_record_part(engine, op, k, user, part, ns);
+    else
+        obs_record_gpu_part(engine, op, k, user, part, ns, staged, moved);
     return 0;
 }
 
@@ -1596,7 +1630,8 @@ encode_split(ecm_ctx_t *ctx, uint64_t nstripes, const void *in, void *const *out
         const uint64_t moved = nstripes * EC_METHOD_CHUNK_SIZE * (ctx->k + ctx->n);
 
         stat_add(ECM_STAT_GPU);
-        obs_record_part(gpu_obs_engine(staged, moved), ECM_ENCODE, ctx->k, user, sg * S, t.ns);
+        obs_record_gpu_part(gpu_obs_engine(staged, moved), ECM_ENCODE, ctx->k, user, sg * S, t.ns,
+                            staged, moved);
         share_learn(ECM_CLS_ENCODE, ECM_ENCODE, ctx->k, ctx->isa, user, moved, staged, nstripes,
                     sg, t.wall, t0);
         return 0;
@@ -1755,7 +1790,8 @@ decode_split(ecm_ctx_t *ctx, const struct dec_call *c, int share, uint64_t stage
         const uint64_t moved = c->nstripes * EC_METHOD_CHUNK_SIZE * (c->k + c->rows);
 
         stat_add(ECM_STAT_GPU);
-        obs_record_part(gpu_obs_engine(staged, moved), ECM_DECODE, c->k, user, sg * per, t.ns);
+        obs_record_gpu_part(gpu_obs_engine(staged, moved), ECM_DECODE, c->k, user, sg * per,
+                            t.ns, staged, moved);
         if (rc == 0)
             share_learn(c->rows == c->k ? ECM_CLS_DECODE : ECM_CLS_PART, ECM_DECODE, c->k,
                         ctx->isa, user, moved, staged, c->nstripes, sg, t.wall, t0);

@@ -374,6 +374,15 @@ int32_t ec_method_xover_plan(uint32_t k, int32_t op, uint64_t user, uint64_t mov
 int32_t ec_method_xover_observe_split(int32_t op, uint32_t k, uint64_t user, uint64_t moved,
                                       uint64_t staged, uint32_t gpu_share, uint64_t gpu_ns,
                                       uint64_t cpu_ns);
+/* One engine's share of a split call as the library records it (r06, tests):
+ * `part` of the call's `user` bytes took `ns` on `engine` (as in
+ * ec_method_xover_observe).  The CPU's share is a sample of its rate inside
+ * calls of `user` bytes; a GPU share, whose time holds the GPU's fixed latency
+ * once, is recorded as the time the whole call would have taken (latency
+ * from `staged` / `moved` as the router models it).  -EINVAL on bad args. */
+int32_t ec_method_xover_observe_part(int32_t engine, int32_t op, uint32_t k, uint64_t user,
+                                     uint64_t part, uint64_t ns, uint64_t staged,
+                                     uint64_t moved);
 int32_t ec_method_xover_observe(int32_t engine, int32_t op, uint32_t k, uint64_t user,
                                 uint64_t ns);
 void ec_method_xover_reset(void);

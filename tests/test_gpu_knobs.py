@@ -10,12 +10,11 @@ EC_MI355X_ZCDB=0 runs host-buffer combines (k <= 8) through the one tile per
 block zero-copy kernel instead of the persistent double-buffered one (the
 default since r04; =1 forces it), each with host encode, decode, heal and
 mixed calls; EC_ZC_TPB (fixed tiles per block) and EC_ZC_INFLIGHT_KB (input
-bytes in flight per round of tiles) size the persistent zero-copy grid;
-EC_MI355X_CHUNK_MB=1 (with LDSNT=1; an A/B knob, off by default) cuts every
-single-pattern device call into launches of 1 MiB of input, ragged last
-launch included; EC_MI355X_TILE_PERM=1 / 2 (A/B, off by default) walk the
-tile encoders' tiles in golden-ratio order / as one contiguous run per XCD.
-Each runs here in its own process through the C ABI, bit-exact against the
+bytes in flight per round of tiles) size the persistent zero-copy grid.
+(r06 retired the measured-negative knobs EC_MI355X_CHUNK_MB,
+EC_MI355X_TILE_PERM and EC_HELPER_SPIN_US from the product: the XCD tile
+order is now a compile-time choice of the >= 4 GiB 16+4 encoder, covered by
+test_gpu_fullsize.py's 4 GiB slices of the 8 GiB job.)  Each runs here in its own process through the C ABI, bit-exact against the
 oracle on device-resident encode, full / partial decode (ragged tiles
 included) and mixed decode.
 """
@@ -118,18 +117,13 @@ print("ok")
 
 KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1"),
          ("EC_MI355X_ZCDB", "0"), ("EC_MI355X_ZCDB", "1"), ("EC_ZC_TPB", "1"), ("EC_ZC_TPB", "16"),
-         ("EC_ZC_INFLIGHT_KB", "64"), ("EC_MI355X_CHUNK_MB", "1"),
-         ("EC_MI355X_TILE_PERM", "1"), ("EC_MI355X_TILE_PERM", "2")]
+         ("EC_ZC_INFLIGHT_KB", "64")]
 
 
 @pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])
 def test_ab_instantiation_bit_exact(knob, value):
     env = dict(os.environ, EC_MI355X_QUIET="1", EC_GPU_ALWAYS="1")
     env[knob] = value
-    if knob == "EC_MI355X_CHUNK_MB":
-        # launches of 1 MiB of input (128-512 stripes): chunking engages on
-        # the non-temporal path only, which these small calls take when forced
-        env["EC_MI355X_LDSNT"] = "1"
     r = subprocess.run([sys.executable, "-c", SCRIPT], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=170)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]

@@ -183,6 +183,37 @@ assert split(8, ENC, 4 * MiB) == e0                   # encode slots untouched
 assert split(8, DEC, 4 * MiB, infl=4 * MiB) < seq[-1]
 L.ec_method_xover_reset()
 assert split(8, DEC, 4 * MiB) != seq[-1] or m0 == seq[-1]
+
+# ADVICE r05 (medium): the samples a split call leaves must not move the
+# routing of whole calls.  Engines: CPU 13 GB/s; GPU 17 GB/s plus the model's
+# 30 us (pinned).  A whole 4 MiB 8+4 decode: CPU 322 us, GPU 277 us -> the GPU.
+# 200 split calls at the balanced share (~51 %) each record both shares; r05
+# recorded the GPU share as part / ns, which charges the 30 us 1 / f times
+# (whole-call estimate 305 us, x1.1 for a near tie > 322: routed to the CPU).
+L.ec_method_xover_reset()
+U, LAT = 4 * MiB, 30000
+cpu_w = int(U / 13.0)                    # ns: 13 GB/s = 13 B/ns
+gpu_w = LAT + int(U / 17.0)
+for _ in range(3):
+    observe(CPU, DEC, 8, U, U / cpu_w)
+    observe(GMAP, DEC, 8, U, U / gpu_w)
+r0, s0 = route(8, DEC, U), split(8, DEC, U)
+p0 = plan(8, DEC, U)
+assert r0 == 0 and 450 <= s0 <= 570, (r0, s0)
+assert L.ec_method_xover_observe_part(CPU, DEC, 8, U, 0, 1, 0, mv) < 0
+assert L.ec_method_xover_observe_part(GMAP, DEC, 8, U, U + 1, 1, 0, mv) < 0
+for _ in range(200):
+    sh = split(8, DEC, U)
+    assert 0 < sh < 1000, sh
+    gp = U * sh // 1000
+    gpu_ns = LAT + int(gp / 17.0)
+    cpu_ns = int((U - gp) / 13.0)
+    assert L.ec_method_xover_observe_part(CPU, DEC, 8, U, U - gp, cpu_ns, 0, mv) == 0
+    assert L.ec_method_xover_observe_part(GMAP, DEC, 8, U, gp, gpu_ns, 0, mv) == 0
+    assert L.ec_method_xover_observe_split(DEC, 8, U, mv, 0, sh, gpu_ns, cpu_ns) == 0
+assert route(8, DEC, U) == r0, "split samples moved whole-call routing"
+assert plan(8, DEC, U) == (p0[0], split(8, DEC, U)), (p0, plan(8, DEC, U))
+assert abs(split(8, DEC, U) - s0) <= 25, (s0, split(8, DEC, U))
 print("OK")
 """
 

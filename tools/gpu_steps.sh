@@ -5,7 +5,7 @@
 # Steps: smoke | pytest | pytest_new (the files in $TESTS) | bench | bench_rocprof
 #        | rehearsal (2 gloo ranks on GPU 0) | profile (per-config rocprof + PMC)
 #        | kbench (tools/kbench/kbench $KBENCH_ARGS) | kb3 (tools/kbench/kb3 $KB3_ARGS)
-#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | zcheal (pinned 16+4 / 8+4 decode, encode, heal, row-masked encode, ZCDB A/B) | fuzz (tools/fuzz_api.py: random calls of every entry point and buffer kind against the oracle, GPU-always then auto) | pcie (DMA copy ceiling of the link, each way and duplex) | zctpb (pinned decodes + encodes 1-256 MiB by EC_ZC_TPB / EC_ZC_INFLIGHT_KB) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | ablib (tools/ab_lib.sh: two library builds alternating through bench.py --only) | concur (tools/kbench/concur: concurrent vs coalesced-ceiling calls, auto / gpu / cpu) | spinab (heal sweep, auto, split helpers polling 0/50/200 us before sleeping) | sharesweep (heal sweep, auto, split share fixed per mille; 0 = the model's) | busyab (heal windows on $BUSY_BUFS buffers from 2/4/8 threads, the busy-staging rule off / on, and CPU-only) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
+#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | zcheal (pinned 16+4 / 8+4 decode, encode, heal, row-masked encode, ZCDB A/B) | fuzz (tools/fuzz_api.py: random calls of every entry point and buffer kind against the oracle, GPU-always then auto) | pcie (DMA copy ceiling of the link, each way and duplex) | zctpb (pinned decodes + encodes 1-256 MiB by EC_ZC_TPB / EC_ZC_INFLIGHT_KB) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | ablib (tools/ab_lib.sh: two library builds alternating through bench.py --only) | concur (tools/kbench/concur: concurrent vs coalesced-ceiling calls, auto / gpu / cpu) | sharesweep (heal sweep, auto, split share fixed per mille; 0 = the model's) | busyab (heal windows on $BUSY_BUFS buffers from 2/4/8 threads, the busy-staging rule off / on, and CPU-only) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
 # Logs go to gpurun_out/${TAG}_<step>.log.
 set -u
 mkdir -p gpurun_out
@@ -44,7 +44,6 @@ for step in "$@"; do
     concur) run concur 400 bash -c 'EC_GPU_ALWAYS=0 tools/kbench/concur ${CONCUR_SECS:-1} auto && EC_GPU_ALWAYS=1 tools/kbench/concur ${CONCUR_SECS:-1} auto && EC_GPU_ALWAYS=0 tools/kbench/concur ${CONCUR_SECS:-1} avx' ;;
     busyab) run busyab 600 bash -c 'for r in 1 2; do for t in ${BUSY_THREADS:-2 4 8}; do for c in 0 10; do echo "== round $r threads $t EC_STAGE_COPY_GBPS=$c"; EC_GPU_ALWAYS=0 EC_STAGE_COPY_GBPS=$c CONCUR_HEAL_THREADS=$t CONCUR_SCEN=heal tools/kbench/concur 1 auto ${BUSY_BUFS:-pageable} || exit 1; done; echo "== round $r threads $t cpu"; EC_GPU_ALWAYS=0 CONCUR_HEAL_THREADS=$t CONCUR_SCEN=heal tools/kbench/concur 1 avx ${BUSY_BUFS:-pageable} || exit 1; done; done' ;;
     sharesweep) run sharesweep 900 bash -c 'for r in 1 2; do for f in ${SHARES:-0 350 450 550 650}; do echo "== round $r EC_HYBRID_SHARE=$f"; EC_GPU_ALWAYS=0 EC_HYBRID_SHARE=$f python3 bench.py --heal-sweep auto --steps 256 || exit 1; done; done' ;;
-    spinab) run spinab 900 bash -c 'for r in 1 2; do for u in ${SPINS:-0 50 200}; do echo "== round $r EC_HELPER_SPIN_US=$u"; EC_GPU_ALWAYS=0 EC_HELPER_SPIN_US=$u python3 bench.py --heal-sweep auto --steps 256 || exit 1; done; done' ;;
     hsauto) run hsauto 900 bash -c 'for r in ${HS_ROUNDS:-1 2 3}; do echo "== round $r"; EC_GPU_ALWAYS=0 python3 bench.py --heal-sweep auto --steps 256 || exit 1; done' ;;
     learnab) run learnab 900 bash -c 'for r in ${HS_ROUNDS:-1 2}; do for l in 0 1; do echo "== round $r EC_SPLIT_LEARN=$l"; EC_GPU_ALWAYS=0 EC_SPLIT_LEARN=$l python3 bench.py --heal-sweep auto --steps 256 || exit 1; done; done' ;;
     ablib) run ablib 900 bash tools/ab_lib.sh "${AB_ARGS:-mixed:8+4 1 mixed:16+4:64 1 dec:8+4:FF0 1}" ;;
