@@ -428,6 +428,10 @@ def extra_configs(c, steps, warmup):
             ex[name] = run_e2e(c, k, n, 512 << 20, 3)
         except Exception as exc:                 # reported, never fatal to the bench line
             ex[name] = dict(error=repr(exc)[:200])
+        # these lines force the GPU path; the library's default
+        # routes host calls (CPU, GPU or split), as heal_sweep / concurrency show
+        ex[name]["engine"] = ("gpu forced (EC_GPU_ALWAYS=%s), not the shipped auto routing"
+                              % os.environ.get("EC_GPU_ALWAYS"))
     try:
         ex["heal_sweep_8+4_4MiB_windows"] = heal_sweep_all()
     except Exception as exc:                     # reported, never fatal to the bench line
@@ -663,32 +667,74 @@ def heal_sweep_all(windows=256):
     return out
 
 
-def concurrency_probe(secs=0.5):
+def concurrency_probe(secs=0.5, rounds=3):
     """The batching-queue question: 8 threads of
     4 MiB 8+4 heal windows and 16 threads of 128 KiB writes / reads through the
     drop-in API on pool buffers (the patched client's iobufs), each timed as
     concurrent calls, as ONE call carrying all their bytes (the ceiling of any
     coalescing queue) and serially -- tools/kbench/concur (C threads: Python's
-    per-call overhead would swamp 4 us CPU calls), per engine setting."""
+    per-call overhead would swamp 4 us CPU calls), per engine setting.
+
+    r06: one 0.5 s run per setting could not separate an
+    effect from box noise, so the engine settings alternate auto / cpu / gpu
+    over `rounds` rounds (the ceiling and serial ways in round 1 only) and the
+    concurrent cells report the median, min and max over the rounds; `verdict`
+    says per scenario whether auto's median beats or trails the CPU engine's by
+    more than the two settings' spread.  `threads` reports the process's
+    threads after a run (main + the library's copy / split-helper threads + the
+    HIP runtime's) beside the copy threads the library sized from the cgroup
+    CPU quota."""
+    import statistics
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "kbench", "concur")
     if not os.path.exists(exe):
         return dict(error="tools/kbench/concur not built (make -C glusterfs_amd tools)")
-    out = {}
-    for mode, gen, always in (("auto", "auto", "0"), ("gpu", "auto", "1"), ("cpu", "avx", "0")):
-        env = dict(os.environ, EC_GPU_ALWAYS=always, EC_MI355X_QUIET="1")
-        r = subprocess.run([exe, str(secs), gen, "pool"], env=env, capture_output=True, text=True,
-                           timeout=240)
-        for line in r.stdout.splitlines():
-            if line.startswith("{"):
+    out = dict(rounds=rounds, secs_per_cell=secs, order="auto, cpu, gpu in every round")
+    cells, threads = {}, {}
+    for rnd in range(rounds):
+        for mode, gen, always in (("auto", "auto", "0"), ("cpu", "avx", "0"), ("gpu", "auto", "1")):
+            env = dict(os.environ, EC_GPU_ALWAYS=always, EC_MI355X_QUIET="1")
+            if rnd:
+                env["CONCUR_WAYS"] = "concurrent"
+            r = subprocess.run([exe, str(secs), gen, "pool"], env=env, capture_output=True,
+                               text=True, timeout=240)
+            for line in r.stdout.splitlines():
+                if not line.startswith("{"):
+                    continue
                 d = json.loads(line)
                 key = "%s_%s" % (d["scenario"], mode)
-                out.setdefault(key, {})[d["way"]] = dict(
-                    user_GBps=d["user_GBps"], p50_us=d["p50_us"], threads=d["threads"],
-                    call_KiB=d["call_KiB"], gpu_calls=d["gpu_calls"], cpu_calls=d["cpu_calls"],
-                    ok=d["ok"])
-        if r.returncode != 0:
-            out["error_" + mode] = (r.stderr or r.stdout)[-300:]
+                cells.setdefault(key, {}).setdefault(d["way"], []).append(d)
+                threads.setdefault(mode, set()).add(d.get("proc_threads"))
+                threads["copy_threads"] = d.get("copy_threads")
+            if r.returncode != 0:
+                out["error_%s_r%d" % (mode, rnd)] = (r.stderr or r.stdout)[-300:]
+    for key, ways in cells.items():
+        o = out.setdefault(key, {})
+        for way, ds in ways.items():
+            v = [d["user_GBps"] for d in ds]
+            o[way] = dict(user_GBps=round(statistics.median(v), 2), user_GBps_min=min(v),
+                          user_GBps_max=max(v), rounds=len(v), p50_us=ds[-1]["p50_us"],
+                          threads=ds[-1]["threads"], call_KiB=ds[-1]["call_KiB"],
+                          gpu_calls=sum(d["gpu_calls"] for d in ds),
+                          cpu_calls=sum(d["cpu_calls"] for d in ds), ok=all(d["ok"] for d in ds))
+    verdict = {}
+    for scen in sorted({k.rsplit("_", 1)[0] for k in cells}):
+        a = out.get(scen + "_auto", {}).get("concurrent")
+        c = out.get(scen + "_cpu", {}).get("concurrent")
+        if not a or not c:
+            continue
+        spread = max(a["user_GBps_max"] - a["user_GBps_min"], c["user_GBps_max"] - c["user_GBps_min"])
+        diff = a["user_GBps"] - c["user_GBps"]
+        verdict[scen] = dict(auto_over_cpu=round(a["user_GBps"] / c["user_GBps"], 3),
+                             diff_GBps=round(diff, 2), spread_GBps=round(spread, 2),
+                             call=("auto ahead" if diff > spread else "auto behind"
+                                   if -diff > spread else "within the spread"))
+    out["verdict"] = verdict
+    hc = host_cpus()
+    out["threads"] = dict(proc_threads_after_run={m: sorted(x for x in v if x is not None)
+                                                  for m, v in threads.items() if m != "copy_threads"},
+                          copy_threads=threads.get("copy_threads"),
+                          cgroup_cpu_quota=hc["cgroup_quota"], affinity_cpus=hc["affinity"])
     return out
 
 
@@ -997,12 +1043,16 @@ def main():
     kt = r["kernel_s"]
     achieved = gbps(2 * r["user"], kt)
 
-    traffic = None
+    traffic, traffic_source = None, None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get("dec_4+2_0x3C_1GiB", {}).get(
-                "hbm_bytes_per_launch")
+            e = json.load(open(tf)).get("dec_4+2_0x3C_1GiB", {})
+            traffic = e.get("hbm_bytes_per_launch")
+            src = e.get("source")
+            traffic_source = dict(src, kernel=e.get("kernel"),
+                                  note="PMC FETCH_SIZE / WRITE_SIZE passes of that profile, "
+                                       "not of this run") if isinstance(src, dict) else src
         except (OSError, ValueError):
             traffic = None
 
@@ -1037,6 +1087,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_source,
             "kernel": "ec_combine_n<K=4,NW=4,MIXED=0,NTS,WOT=1> (decode: 4-stripe tiles, "
                       "jump-table multiply, per-wave 512-B output runs)",
             "algorithmic_bytes_per_launch": 2 * r["user"],

@@ -275,7 +275,11 @@ const char *ec_method_engine(const ec_matrix_list_t *list);
 
 /* Process-wide engine counters: host-buffer calls coded on a GPU, calls
  * coded by the CPU engine, and, among the latter, fallbacks after a failed
- * device submission. */
+ * device submission.  A split call (r05: a GPU codes the first share of its
+ * stripes, the calling thread's CPU engine the rest) adds 1 to both
+ * gpu_calls and cpu_calls, so gpu_calls + cpu_calls counts engine runs, not
+ * API calls; when its GPU share fails and is redone on the CPU engine,
+ * cpu_fallbacks goes up and cpu_calls stays as the split left it. */
 typedef struct {
     uint64_t gpu_calls;
     uint64_t cpu_calls;
@@ -286,7 +290,14 @@ void ec_method_get_stats(ec_method_stats_t *stats);
  * host-buffer device submissions fail with -EIO before touching a device,
  * so the CPU fallback runs. */
 void ec_method_inject_device_faults(uint32_t count);
-/* Why the calling thread's last failing call failed (diagnostics): the
+/* HIP errors and the caller: every device entry point first clears any
+ * non-sticky HIP error left pending on the calling thread
+ * (hipGetLastError), so that its own launch checks see only its own
+ * launches.  A caller that shares the thread's HIP runtime (torch, a
+ * client's own kernels) must read its own pending error before calling in:
+ * the library consumes it, and records it nowhere.
+ *
+ * Why the calling thread's last failing call failed (diagnostics): the
  * device layer's record (the HIP call or kernel and its error), or the
  * entry point and errno of a failure it did not record (an argument error).
  * Per thread: a client's epoll threads each read their own.  The text stays

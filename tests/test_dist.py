@@ -157,3 +157,74 @@ def test_bind_to_node(tmp_path):
         assert bind_to_node(0, sysfs=str(tmp_path)) == set(pick)
     finally:
         os.sched_setaffinity(0, aff)
+
+
+def _eight_rank_worker(rank, world, port, q):
+    """One of 8 gloo ranks of configs[3]'s strong job: the
+    rank's placement as bench.py's bind_rank makes it, with the GPU pool's
+    16-CPU quota split 8 ways, then its 1 GiB slice of the 8 GiB job --
+    generated alone by jump-ahead, encoded by the product's CPU engine -- and
+    its input and 20 fragments against the slice's SHA-256 fixture."""
+    import hashlib
+    import importlib.util
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), EC_MI355X_QUIET="1")
+    os.environ.pop("EC_COPY_THREADS", None)
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    import glusterfs_amd as g
+    from glusterfs_amd import synth
+    from glusterfs_amd.dist import Group, stripe_range
+
+    # the pool's quota (16 CPUs for all ranks of a node), whatever this host has
+    real = bench.host_cpus
+    bench.host_cpus = lambda: dict(real(), cgroup_quota=16, threads=16)
+    placement = bench.bind_rank(g, rank, world)
+    copy_env = os.environ.get("EC_COPY_THREADS")
+    fx = json.load(open(os.path.join(root, "tests", "golden", "fullsize_sha256.json")))
+    case = fx["cases"]["16+4_8GiBjob_N%d_r%d" % (world, rank)]
+    k, n = 16, 20
+    grp = Group(backend="gloo")
+    s0, s1 = stripe_range(grp.rank, grp.world, bench.STRONG_STRIPES)
+    ok = (s1 - s0) * 512 * k == case["bytes"]
+    data = synth.fill_numpy((s1 - s0) * 512 * k, word0=s0 * 512 * k // 8)
+    ok &= hashlib.sha256(data).hexdigest() == case["data"]
+    frags = [np.empty((s1 - s0) * 512, np.uint8) for _ in range(n)]
+    with g.ECMatrixList(k, n, gen="avx") as L:
+        L.encode_batch(s1 - s0, data, frags)
+    del data
+    ok &= [hashlib.sha256(f).hexdigest() for f in frags] == case["frags"]
+    del frags
+    ok_all = grp.all_ok(ok)
+    grp.close()
+    q.put((rank, ok, ok_all, s0, s1, copy_env, placement["copy_threads"]))
+
+
+def test_eight_rank_strong_job_fixtures():
+    """N = 8 rehearsed on the CPU before the driver's first 8-GPU run: eight
+    gloo ranks, the 8 GiB configs[3] job cut into eight 1 GiB slices, each
+    slice's input and fragments against its own fixture; bind_rank gives
+    every rank 16 / 8 = 2 copy threads."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 8
+    ps = [ctx.Process(target=_eight_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] for r in res), [r[:2] for r in res]       # each slice vs its fixture
+    assert all(r[2] for r in res)                              # and the all-ranks flag
+    assert res[0][3] == 0 and res[-1][4] == 1 << 20
+    assert all(a[4] == b[3] for a, b in zip(res, res[1:]))     # contiguous, disjoint
+    assert all(r[5] == "2" for r in res), [r[5] for r in res]  # 16 CPUs / 8 ranks
+    assert all(r[6] == 2 for r in res), [r[6] for r in res]    # as the library applies it

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "glusterfs_amd", "csrc")
 
 
-def build(tmp_path, san):
+def build(tmp_path, san, main="sanitize_check"):
     cc = shutil.which("gcc")
     if cc is None:
         pytest.skip("gcc not installed")
@@ -37,8 +37,8 @@ def build(tmp_path, san):
                                        "-o", o]))
         objs.append(o)
     assert all(p.wait() == 0 for p in procs)
-    exe = str(tmp_path / "sanitize_check")
-    subprocess.run([cc, *common, os.path.join(ROOT, "tests", "c", "sanitize_check.c"), *objs,
+    exe = str(tmp_path / main)
+    subprocess.run([cc, *common, os.path.join(ROOT, "tests", "c", main + ".c"), *objs,
                     "-o", exe], check=True)
     return exe
 
@@ -60,3 +60,16 @@ def test_host_layer_under_sanitizers(tmp_path, san):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0 and "failures=0" in r.stdout, (r.stdout + r.stderr)[-4000:]
     assert "split calls" in r.stdout, r.stdout[-2000:]
+
+
+def test_fork_after_split_calls(tmp_path):
+    """a child forked after the parent's split calls starts
+    its own split helpers (pthread_atfork), instead of queueing its GPU share
+    for the parent's helper threads, which it does not have, and waiting
+    forever.  Stub device, every >= 1 MiB call split; tests/c/fork_check.c."""
+    exe = build(tmp_path, ["-O1"], main="fork_check")
+    env = dict(os.environ, EC_MI355X_QUIET="1", ECD_STUB_GPU="1", EC_HYBRID_SHARE="450",
+               EC_CPU_ENC_GBPS_K2="6", EC_CPU_DEC_GBPS_K="4")
+    env.pop("EC_GPU_ALWAYS", None)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "parent ok, child exit 0" in r.stdout, r.stdout + r.stderr

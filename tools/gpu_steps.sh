@@ -28,7 +28,7 @@ for step in "$@"; do
     bench_rocprof) run bench_rocprof 300 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_bench_$TAG -o run --output-format csv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-extra --no-cpu && python3 $R/tools/prof_filter.py $R/gpurun_out/prof_bench_$TAG ec_" ;;
     rehearsal) run rehearsal 300 env EC_BENCH_BACKEND=gloo EC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1 ;;
     rehearsal4) run rehearsal4 600 env EC_BENCH_BACKEND=gloo EC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 4 --steps 3 --warmup 1 ;;
-    profile) run profile 900 bash tools/profile.sh "$TAG" ${PROFILE_ARGS:-dec:4+2:3C 1 enc:4+2 1 enc:8+4 0.25 dec:8+4:FF0 0.25 enc:16+4 2 mixed:8+4 1 heal:8+4 1 dec:16+4:FFFF0 1 mixed:16+4:64 1 rmw:4+2 1} ;;
+    profile) run profile 900 bash tools/profile.sh "$TAG" ${PROFILE_ARGS:-dec:4+2:3C 1 enc:4+2 1 enc:8+4 0.25 dec:8+4:FF0 0.25 enc:16+4 2 mixed:8+4 1 heal:8+4 1 dec:16+4:FFFF0 1 mixed:16+4:64 1 rmw:4+2 1 rmw:8+4 1 rmw:16+4 1} ;;
     kbench) run kbench 600 tools/kbench/kbench ${KBENCH_ARGS:-} ;;
     trace) run trace 600 bash tools/prof_trace.sh "$TAG" ${TRACE_ARGS:-dec:16+4:FFFF0 1 dec:4+2:3C 1} ;;
     zcab) run zcab 600 bash -c 'for r in 1 2 3; do for v in 0 1; do echo "== round $r EC_MI355X_ZCDB=$v"; EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v python3 bench.py --heal-sweep gpu --steps 256 || exit 1; done; done' ;;

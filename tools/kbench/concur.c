@@ -23,7 +23,10 @@
  *       -lec_mi355x -Wl,-rpath,'$ORIGIN/../../glusterfs_amd/lib' -o tools/kbench/concur
  *   tools/kbench/concur [secs] [gen] [pool|pageable|both]
  *   (CONCUR_HEAL_THREADS: heal threads, default 8; CONCUR_SCEN=heal|write|read:
- *   that scenario only)                                                   */
+ *   that scenario only; CONCUR_WAYS=concurrent,ceiling,serial: those ways only)
+ * Each line also reports the process's threads after the run (the library's
+ * copy / helper threads and the HIP runtime's, plus main) and the copy
+ * threads the library sized from the CPU quota.                                                   */
 #define _GNU_SOURCE
 #include <pthread.h>
 #include <sched.h>
@@ -31,9 +34,24 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dirent.h>
 #include <time.h>
 
 #include "ec_method.h"
+
+/* threads of this process now (after the workers were joined: the main
+ * thread plus every thread the library and the HIP runtime started) */
+static int proc_threads(void)
+{
+    DIR *d = opendir("/proc/self/task");
+    int n = 0;
+    if (!d)
+        return -1;
+    for (struct dirent *e; (e = readdir(d));)
+        n += e->d_name[0] != '.';
+    closedir(d);
+    return n;
+}
 
 static double now(void)
 {
@@ -192,12 +210,13 @@ static int run(ec_matrix_list_t *list, const char *way, int scen, int pool, size
     printf("{\"scenario\": \"%s\", \"mode\": \"%s\", \"buffers\": \"%s\", \"way\": \"%s\", "
            "\"threads\": %d, \"call_KiB\": %zu, \"user_GBps\": %.2f, \"calls_per_s\": %.0f, "
            "\"p50_us\": %.1f, \"p99_us\": %.1f, \"gpu_calls\": %llu, \"cpu_calls\": %llu, "
-           "\"ok\": %s}\n",
+           "\"proc_threads\": %d, \"copy_threads\": %d, \"ok\": %s}\n",
            scen_name[scen], mode, pool ? "pool" : "pageable", way, threads, size >> 10,
            (double)calls * size / secs / 1e9, calls / secs, nl ? all[nl / 2] * 1e6 : 0.0,
            nl ? all[(long)(nl * 0.99)] * 1e6 : 0.0,
            (unsigned long long)(s1.gpu_calls - s0.gpu_calls),
-           (unsigned long long)(s1.cpu_calls - s0.cpu_calls), bad ? "false" : "true");
+           (unsigned long long)(s1.cpu_calls - s0.cpu_calls), proc_threads(),
+           ec_method_copy_threads(), bad ? "false" : "true");
     fflush(stdout);
     free(all);
     return bad;
@@ -240,6 +259,13 @@ static void bind_gpu_node(void)
         fprintf(stderr, "concur: bound to %d CPUs of node %d\n", CPU_COUNT(&want), node);
 }
 
+/* CONCUR_WAYS: comma-separated ways to run (default all three) */
+static int way_on(const char *way)
+{
+    const char *e = getenv("CONCUR_WAYS");
+    return !e || !*e || strstr(e, way) != NULL;
+}
+
 int main(int argc, char **argv)
 {
     bind_gpu_node();
@@ -266,10 +292,13 @@ int main(int argc, char **argv)
                 continue;
             if (only && strncmp(scen_name[sc[s].scen], only, strlen(only)))
                 continue;
-            bad |= run(&list, "concurrent", sc[s].scen, pool, sc[s].size, threads, secs, mode);
-            bad |= run(&list, "ceiling", sc[s].scen, pool, sc[s].size * threads, 1, secs,
-                       mode);
-            bad |= run(&list, "serial", sc[s].scen, pool, sc[s].size, 1, secs, mode);
+            if (way_on("concurrent"))
+                bad |= run(&list, "concurrent", sc[s].scen, pool, sc[s].size, threads, secs, mode);
+            if (way_on("ceiling"))
+                bad |= run(&list, "ceiling", sc[s].scen, pool, sc[s].size * threads, 1, secs,
+                           mode);
+            if (way_on("serial"))
+                bad |= run(&list, "serial", sc[s].scen, pool, sc[s].size, 1, secs, mode);
         }
     ec_method_fini(&list);
     return bad;

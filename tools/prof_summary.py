@@ -67,7 +67,7 @@ def main():
     # GiB per config as tools/gpu_final.sh passes them
     gib = {"dec_4p2_3C": 1, "enc_4p2": 1, "enc_8p4": 0.25, "dec_8p4_FF0": 0.25,
            "enc_16p4": 2, "dec_8p4_EB5": 0.25, "dec_4p2_0F": 1, "mixed_8p4": 1, "heal_8p4": 1,
-           "dec_16p4_FFFF0": 1, "mixed_16p4_64": 1, "rmw_4p2": 1}
+           "dec_16p4_FFFF0": 1, "mixed_16p4_64": 1, "rmw_4p2": 1, "rmw_8p4": 1, "rmw_16p4": 1}
     # overrides: PROF_GIB="dec_8p4_FF0=1,..." (a config profiled at another size)
     for kv in filter(None, os.environ.get("PROF_GIB", "").split(",")):
         name, val = kv.split("=")
@@ -114,8 +114,22 @@ def main():
     open(dst + "_summary.md", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
     if traffic_path:
+        # provenance of every entry: the profile, the commit
+        # the profiled tree was at (this runs in the git checkout, after the
+        # GPU run merged its output back) and when it was summarised
+        import datetime
+        import subprocess
+        try:
+            commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True,
+                                    text=True, cwd=os.path.dirname(os.path.abspath(__file__))
+                                    ).stdout.strip() or None
+        except OSError:
+            commit = None
+        prov = dict(profile=os.path.basename(src.rstrip("/")), summary=dst + "_summary.md",
+                    commit=os.environ.get("PROF_COMMIT", commit),
+                    date=datetime.date.today().isoformat())
         keymap = {"dec_4p2_3C": "dec_4+2_0x3C_1GiB"}
-        tj = {keymap.get(k, k): v for k, v in traffic.items()}
+        tj = {keymap.get(k, k): dict(v, source=prov) for k, v in traffic.items()}
         json.dump(tj, open(traffic_path, "w"), indent=1)
 
 
