@@ -16,6 +16,8 @@ from .ec_method import (  # noqa: F401
     gf_div,
     gf_mul,
     host_registered,
+    jit_compile_check,
+    jit_stats,
     inject_device_faults,
     inverse_matrix,
     mask_rows,

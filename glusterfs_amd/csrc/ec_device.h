@@ -159,6 +159,18 @@ typedef struct ecd_pool_stats {
 } ecd_pool_stats_t;
 void ecd_pool_stats(ecd_pool_stats_t *s);
 
+/* Per-pattern whole-matrix kernels compiled at run time (ec_jit.hip, r06). */
+typedef struct ecd_jit_stats {
+    uint64_t compiled, failed, launches, compile_us, lookups, entries;
+} ecd_jit_stats_t;
+void ecd_jit_stats(ecd_jit_stats_t *s);
+/* Generate and compile the kernel of one coefficient matrix (rows x k bytes)
+ * without loading it: its code size, or -errno (-ENOSYS without hiprtc);
+ * *ops = v_xor / v_bitop3 instructions per dword column; log = compiler
+ * output on failure. */
+int ecd_jit_compile_check(uint32_t k, uint32_t rows, const uint8_t *coef, uint32_t *ops,
+                          char *log, size_t log_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,6 +39,7 @@
 
 #include "ec_kernels.h"
 #include "ec_kernels_impl.h"
+#include "ec_jit.h"
 
 using namespace ecdev;
 
@@ -855,8 +856,21 @@ int ecdk_pack_args(const ecd_combine_desc_t *d, CombineArgs *a)
  * takes any source alignment (tools/kbench/ldsdma_align.hip,
  * profiles/r03/ldsdma_align.log): fragments at odd offsets (torch slices)
  * are read in place.  (Round 2 copied them to aligned scratch first.) */
+/* A single-pattern combine of a wide code whose coefficient matrix has a
+ * compiled whole-matrix kernel (ec_jit.hip, r06) runs that; every other
+ * call, and the calls of a matrix whose code is still being compiled, run
+ * the shipped kernels. */
 int ecdk_combine(hipStream_t s, const ecd_combine_desc_t *d)
 {
+    if (ecj_eligible(d)) {
+        uintptr_t o = (uintptr_t)d->in_stride;
+        const uint8_t *pat = d->pat_ext ? d->pat_ext : d->pat;
+        for (u32 p = 0; p < d->k; ++p)
+            o |= (uintptr_t)d->in_base[pat[p]];
+        const bool nt = nt_staging(d->nstripes * d->k * ECD_CHUNK) && (o & 15u) == 0;
+        if (ecj_launch(s, d, nt) == 0)
+            return 0;
+    }
     return combine_any<true>(s, d);
 }
 

@@ -1484,6 +1484,30 @@ ec_method_pool_stats(ec_method_pool_stats_t *st)
     st->unregister_us = s.unregister_us;
 }
 
+void
+ec_method_jit_stats(ec_method_jit_stats_t *st)
+{
+    ecd_jit_stats_t s;
+
+    if (!st)
+        return;
+    ecd_jit_stats(&s);
+    st->compiled = s.compiled;
+    st->failed = s.failed;
+    st->launches = s.launches;
+    st->compile_us = s.compile_us;
+    st->lookups = s.lookups;
+    st->entries = s.entries;
+}
+
+int32_t
+ec_method_jit_compile_check(uint32_t k, uint32_t rows, const uint8_t *coef, uint32_t *ops)
+{
+    char log[512];
+
+    return ecd_jit_compile_check(k, rows, coef, ops, log, sizeof log);
+}
+
 /* disperse.cpu-extensions (ec.c:1786-1794) -> engine.  The reference maps
  * none to portable C and x64 / sse / avx to its JIT back ends, auto to the
  * best of them (ec-code.c:59-69, 977-1060).  Here auto (and hip) select the

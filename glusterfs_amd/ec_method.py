@@ -43,7 +43,8 @@ EXPORTS = (
     "ec_method_writev_encode_device", "ec_method_engine", "ec_method_get_stats",
     "ec_method_inject_device_faults", "ec_method_device_numa_node", "ec_method_copy_threads",
     "ec_method_host_register_async", "ec_method_host_register_flush", "ec_method_buffer_get",
-    "ec_method_buffer_put", "ec_method_pool_stats", "ec_method_xover_route",
+    "ec_method_buffer_put", "ec_method_pool_stats", "ec_method_jit_stats",
+    "ec_method_jit_compile_check", "ec_method_xover_route",
     "ec_method_xover_split",
     "ec_method_xover_plan",
     "ec_method_xover_observe_split",
@@ -91,6 +92,12 @@ class Stats(ctypes.Structure):
     """ec_method_stats_t: process-wide engine counters."""
     _fields_ = [("gpu_calls", ctypes.c_uint64), ("cpu_calls", ctypes.c_uint64),
                 ("cpu_fallbacks", ctypes.c_uint64)]
+
+
+class JitStats(ctypes.Structure):
+    """ec_method_jit_stats_t: per-pattern kernels compiled at run time."""
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("compiled", "failed", "launches", "compile_us", "lookups", "entries")]
 
 
 class PoolStats(ctypes.Structure):
@@ -166,6 +173,8 @@ def _load():
         "ec_method_buffer_get": (vp, [ctypes.c_size_t]),
         "ec_method_buffer_put": (i32, [vp]),
         "ec_method_pool_stats": (None, [ctypes.POINTER(PoolStats)]),
+        "ec_method_jit_stats": (None, [ctypes.POINTER(JitStats)]),
+        "ec_method_jit_compile_check": (i32, [u32, u32, vp, ctypes.POINTER(u32)]),
         "ec_method_xover_route": (i32, [u32, i32, u64, u64, u64, u64]),
         "ec_method_xover_split": (i32, [u32, i32, u64, u64, u64, u64]),
         "ec_method_xover_plan": (i32, [u32, i32, u64, u64, u64, u64, u32, ctypes.POINTER(i32)]),
@@ -244,6 +253,23 @@ def stats():
     st = Stats()
     lib.ec_method_get_stats(ctypes.byref(st))
     return dict(gpu_calls=st.gpu_calls, cpu_calls=st.cpu_calls, cpu_fallbacks=st.cpu_fallbacks)
+
+
+def jit_stats():
+    """Counters of the run-time compiled whole-matrix kernels."""
+    st = JitStats()
+    lib.ec_method_jit_stats(ctypes.byref(st))
+    return {n: getattr(st, n) for n, _ in JitStats._fields_}
+
+
+def jit_compile_check(k, rows, coef):
+    """Compile (without a device) the kernel of a rows x k coefficient matrix:
+    (code bytes or -errno, XOR instructions per dword column)."""
+    import numpy as np
+    c = np.ascontiguousarray(np.asarray(coef, dtype=np.uint8).reshape(rows, k))
+    ops = ctypes.c_uint32(0)
+    rc = lib.ec_method_jit_compile_check(k, rows, c.ctypes.data, ctypes.byref(ops))
+    return rc, ops.value
 
 
 def pool_stats():

@@ -414,6 +414,33 @@ typedef struct {
 } ec_method_pool_stats_t;
 void ec_method_pool_stats(ec_method_pool_stats_t *stats);
 
+/* Per-pattern kernels compiled at run time (r06; the counterpart of the
+ * reference's per-row JIT, ec-code.c:722-809).  A device-buffer combine with
+ * one erasure pattern of a wide code (k >= 12 data and >= 12 output rows,
+ * e.g. a 16+4 decode; >= EC_MI355X_JIT_MIN_STRIPES stripes, default 1024)
+ * queues its coefficient matrix for compilation (hiprtc, opened with dlopen;
+ * one library thread, ~1-2 s) as one straight-line XOR program over the
+ * whole matrix, and runs the shipped kernel until that code exists; later
+ * calls of the matrix run it.  Results are identical either way.
+ * EC_MI355X_JIT=0 turns this off, EC_MI355X_JIT_SYNC=1 compiles on the
+ * calling thread.  Counters: */
+typedef struct {
+    uint64_t compiled;    /* matrices compiled                          */
+    uint64_t failed;      /* compilations that failed (shipped kernel)  */
+    uint64_t launches;    /* calls that ran a compiled kernel           */
+    uint64_t compile_us;  /* time spent compiling                       */
+    uint64_t lookups;     /* eligible calls                             */
+    uint64_t entries;     /* matrices in the cache now (<= 32)          */
+} ec_method_jit_stats_t;
+void ec_method_jit_stats(ec_method_jit_stats_t *stats);
+/* Generate and compile (without loading) the kernel of a rows x k matrix of
+ * GF(2^8) coefficients (row-major): returns its code size in bytes, or
+ * -errno (-ENOSYS without hiprtc, -EIO when the compiler failed); *ops, when
+ * not NULL, gets the program's XOR instructions per dword column.  Needs no
+ * device (tests). */
+int32_t ec_method_jit_compile_check(uint32_t k, uint32_t rows, const uint8_t *coef,
+                                    uint32_t *ops);
+
 /* Host-side matrix helpers, exported for tests and tools: the n x k encode
  * matrix (ec-method.c:22-36) and the k x k inverse for ascending rows
  * (ec-method.c:38-72), as uint32 values in [0, 255].  Return 0 or -EINVAL. */

@@ -118,3 +118,6 @@ void ecd_inject_faults(uint32_t n) { (void)n; }
 int ecd_host_mapped(const void *p, size_t n) { (void)p; (void)n; return stub_gpu(); }
 int ecd_device_numa_node(int d) { (void)d; return -ENODEV; }
 int ecd_copy_threads(void) { return 0; }
+void ecd_jit_stats(ecd_jit_stats_t *s) { memset(s, 0, sizeof(*s)); }
+int ecd_jit_compile_check(uint32_t k, uint32_t r, const uint8_t *c, uint32_t *o, char *l, size_t n)
+{ (void)k; (void)r; (void)c; (void)o; (void)l; (void)n; return -ENOSYS; }

@@ -12,6 +12,9 @@
 
 /* ec_device.hip's error record, which the launchers call (not linked here) */
 extern "C" int ecd_hip_fail(const char *, int) { return -EIO; }
+/* the run-time compiled kernels (ec_jit.hip) are not part of this harness */
+extern "C" int ecj_eligible(const ecd_combine_desc_t *) { return 0; }
+extern "C" int ecj_launch(hipStream_t, const ecd_combine_desc_t *, int) { return -EAGAIN; }
 
 #include <algorithm>
 #include <cstdio>
@@ -252,6 +255,99 @@ static void add_combine_ct(std::vector<Variant> &v, const char *nm, const Combin
     v.push_back({nm, bytes, [=](hipStream_t st) {
                      hipLaunchKernelGGL(kern, dim3((u32)g), dim3(64 * NW), lds, st, *a);
                  }, out, ob});
+}
+
+/* r06: the whole-matrix program of ONE fixed 16 x 16
+ * decode matrix (kb3's dense ct_coef matrix), four-Russians over 4-plane
+ * groups with the sub-sums shared by all 128 output planes
+ * (tools/gen/gen_wm16.py -> kb_wm16.h: 2381 instructions per dword column
+ * against 3290 for the row-by-row programs).  One 4-stripe tile per block
+ * (32 KiB of LDS, staged by LDS-DMA like the shipped kernels); each lane
+ * owns one dword column of the 4 stripes.  NWV = 1: one wave runs all 16
+ * rows (128 accumulators); NWV = 2: two waves run 8 rows each (the tables
+ * built twice, 2725 instructions).  The outputs of a full decode are one
+ * contiguous 32 KiB run per tile (stripe-major), so they go back through
+ * the tile's LDS and leave as 16-byte lane stores.  MODE 1: compute only
+ * (no staging, no stores) -- the time of the program itself. */
+#include "kb_wm16.h"
+
+template <int NWV, int MODE, int LA>
+__global__ __launch_bounds__(NWV * 64) void kb_combine_wm(const CombineArgs a)
+{
+    constexpr int T = 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    if constexpr (MODE == 0)
+        stage_tile<T, NWV, LA>(lds, [&](u32 p, uint64_t st) {
+            return a.in_base[p] + st * a.in_stride;
+        }, 16, t0, a.nstripes, wave, lane);
+    __syncthreads();
+    const u32 cs = lane >> 4, cc = lane & 15u;
+    const uint8_t *col = lds + cs * 64u + cc * 4u;
+    uint8_t *ob = lds + cs * 8192u + cc * 4u;
+    if constexpr (NWV == 1) {
+        u32 acc[128];
+        wm16_rows16<T>(col, acc);
+        if constexpr (MODE == 1) {
+            u32 x = 0;
+#pragma unroll
+            for (int o = 0; o < 128; ++o)
+                x ^= acc[o];
+            if (x == 0x9E3779B9u)             /* keeps the program live */
+                *reinterpret_cast<u32 *>(a.out_base[0]) = x;
+            return;
+        }
+        /* LDS operations of one wave run in order: the input tile is read
+         * before it is overwritten */
+#pragma unroll
+        for (int o = 0; o < 128; ++o)
+            *reinterpret_cast<u32 *>(ob + (o >> 3) * 512u + (o & 7) * 64u) = acc[o];
+    } else {
+        u32 acc[64];
+        if (wave == 0)
+            wm16_rows_lo<T>(col, acc);
+        else
+            wm16_rows_hi<T>(col, acc);
+        if constexpr (MODE == 1) {
+            u32 x = 0;
+#pragma unroll
+            for (int o = 0; o < 64; ++o)
+                x ^= acc[o];
+            if (x == 0x9E3779B9u)
+                *reinterpret_cast<u32 *>(a.out_base[0]) = x;
+            return;
+        }
+        __syncthreads();                       /* both waves done reading */
+#pragma unroll
+        for (int o = 0; o < 64; ++o)
+            *reinterpret_cast<u32 *>(ob + (wave * 8 + (o >> 3)) * 512u + (o & 7) * 64u) = acc[o];
+    }
+    __syncthreads();
+    uint8_t *o = a.out_base[0] + t0 * a.out_stride;
+    const uint64_t left = a.nstripes - t0;
+    const u32 nbytes = (u32)(left < T ? left : T) * 8192u;
+#pragma unroll 4
+    for (u32 i = tid * 16u; i < (u32)T * 8192u; i += NWV * 64u * 16u)
+        if (i < nbytes)
+            __builtin_nontemporal_store(*reinterpret_cast<const v4u *>(lds + i),
+                                        reinterpret_cast<v4u *>(o + i));
+}
+
+template <int NWV, int MODE>
+static void add_combine_wm(std::vector<Variant> &v, const char *nm, const CombineArgs *a,
+                           double bytes, uint8_t *out, size_t ob)
+{
+    const bool nt = nt_staging(a->nstripes * 16 * ECD_CHUNK);
+    const void *kern = nt ? (const void *)kb_combine_wm<NWV, MODE, kLdsDmaNT>
+                          : (const void *)kb_combine_wm<NWV, MODE, kLdsDmaDefault>;
+    const uint64_t g = (a->nstripes + 3) / 4;
+    v.push_back({nm, bytes, [=](hipStream_t st) {
+                     void *args[] = {(void *)a};
+                     CHK(hipLaunchKernel(kern, dim3((u32)g), dim3(64 * NWV), args, 32u << 10, st));
+                 }, MODE == 0 ? out : nullptr, ob});
 }
 
 /* Double-buffered persistent combine for k = 16 (r03 candidate, measured slower: DESIGN.md 3.3.1).  The 8-stripe
@@ -1001,6 +1097,37 @@ int main(int argc, char **argv)
         add_combine_ct<K, 4, 4, true>(v, "ct T4 NW4 WOT", a, bytes, bufB, ob);
         add_combine_ct<K, 4, 8, false>(v, "ct T4 NW8", a, bytes, bufB, ob);
         run_group("decode 16+4 dense, compile-time matrix", v, rounds, iters, s);
+        v.clear();
+    }
+    if (want(groups, "dec16wm")) {  /* whole-matrix program (r06) */
+        constexpr int K = 16;
+        const uint64_t nst = user / (K * ECD_CHUNK);
+        uint8_t *fr[16];
+        for (int p = 0; p < K; ++p)
+            fr[p] = bufA + (uint64_t)p * nst * ECD_CHUNK;
+        uint8_t c[256];
+        for (int i = 0; i < 256; ++i)
+            c[i] = (uint8_t)ct_coef(i);
+        const CombineArgs *a = make_args(K, K, nst, fr, bufB, true, c);
+        const double bytes = 2.0 * nst * K * ECD_CHUNK;
+        const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        printf("instructions per dword column: row by row %d, whole matrix %d, two halves %d\n",
+               WM16_OPS_ROWWISE, WM16_OPS_FULL, WM16_OPS_HALVES);
+        add_shipped_combine(v, "shipped (run-time matrix)", a, bytes, bufB, ob);
+        add_combine_wm<1, 0>(v, "whole matrix, 1 wave x 16 rows", a, bytes, bufB, ob);
+        add_combine_wm<2, 0>(v, "whole matrix, 2 waves x 8 rows", a, bytes, bufB, ob);
+        add_combine_ct<K, 4, 4, true>(v, "ct row-wise T4 NW4 WOT", a, bytes, bufB, ob);
+        add_combine_wm<1, 1>(v, "whole matrix 16 rows, compute only", a, bytes, bufB, ob);
+        add_combine_wm<2, 1>(v, "whole matrix 2 x 8 rows, compute only", a, bytes, bufB, ob);
+        {
+            const uint64_t g = (a->nstripes + 7) / 8;
+            const void *kern = (const void *)kb_combine_probe<7>;
+            v.push_back({"shipped, compute only (probe 7)", bytes, [=](hipStream_t st) {
+                             void *args[] = {(void *)a};
+                             CHK(hipLaunchKernel(kern, dim3((u32)g), dim3(1024), args, 64u << 10, st));
+                         }, nullptr, ob});
+        }
+        run_group("decode 16+4 dense, whole-matrix program (r06)", v, rounds, iters, s);
         v.clear();
     }
     if (want(groups, "dec8"))
