@@ -319,9 +319,12 @@ struct Rtc {
 
     Rtc()
     {
-        void *h = dlopen("libhiprtc.so.7", RTLD_NOW | RTLD_LOCAL);
-        if (!h)
-            h = dlopen("libhiprtc.so", RTLD_NOW | RTLD_LOCAL);
+        /* the loader's path first (a process that already mapped a hiprtc,
+         * e.g. torch's, gets that one), then the ROCm install */
+        void *h = nullptr;
+        for (const char *n : {"libhiprtc.so.7", "libhiprtc.so", "/opt/rocm/lib/libhiprtc.so.7"})
+            if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL)))
+                break;
         if (!h) {
             why = "libhiprtc not found";
             return;
@@ -567,6 +570,10 @@ struct JitArgs {
 
 } // namespace
 
+/* development hook (tools/kbench/kb3.hip): extra LDS per block, to trade
+ * blocks per CU against the tile in A/B runs; 0 in the library */
+extern "C" int ecj_lds_pad_kb = 0;
+
 extern "C" int ecj_eligible(const ecd_combine_desc_t *d)
 {
     if (!jit_on() || d->npatterns != 1 || d->group_pattern || d->k < 12 || d->k > ECJ_MAX ||
@@ -613,7 +620,8 @@ extern "C" int ecj_launch(hipStream_t s, const ecd_combine_desc_t *d, int nt)
     a.contig = d->out_stride == (uint64_t)d->rows * 512;
     for (uint32_t r = 1; r < d->rows && a.contig; ++r)
         a.contig = a.out[r] == a.out[0] + (size_t)r * 512;
-    const size_t lds = (size_t)(d->k > d->rows ? d->k : d->rows) * 4 * 512;
+    const size_t lds = (size_t)(d->k > d->rows ? d->k : d->rows) * 4 * 512 +
+                       (size_t)ecj_lds_pad_kb * 1024;
     void *params[] = {&a};
     const hipError_t rc = hipModuleLaunchKernel(f, (u32)((d->nstripes + 3) / 4), 1, 1, 128, 1, 1,
                                                 (u32)lds, s, params, nullptr);

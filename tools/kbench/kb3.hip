@@ -12,9 +12,14 @@
 
 /* ec_device.hip's error record, which the launchers call (not linked here) */
 extern "C" int ecd_hip_fail(const char *, int) { return -EIO; }
-/* the run-time compiled kernels (ec_jit.hip) are not part of this harness */
+#ifdef KB3_WITH_JIT
+extern "C" int ecj_lds_pad_kb;
+#else
+/* the run-time compiled kernels (ec_jit.hip) are not part of this harness
+ * unless it is built with them (-DKB3_WITH_JIT ../../glusterfs_amd/csrc/ec_jit.hip -ldl) */
 extern "C" int ecj_eligible(const ecd_combine_desc_t *) { return 0; }
 extern "C" int ecj_launch(hipStream_t, const ecd_combine_desc_t *, int) { return -EAGAIN; }
+#endif
 
 #include <algorithm>
 #include <cstdio>
@@ -1117,6 +1122,46 @@ int main(int argc, char **argv)
         add_combine_wm<1, 0>(v, "whole matrix, 1 wave x 16 rows", a, bytes, bufB, ob);
         add_combine_wm<2, 0>(v, "whole matrix, 2 waves x 8 rows", a, bytes, bufB, ob);
         add_combine_ct<K, 4, 4, true>(v, "ct row-wise T4 NW4 WOT", a, bytes, bufB, ob);
+#ifdef KB3_WITH_JIT
+        {
+            /* the library's path: ecdk_combine -> the hiprtc-compiled kernel
+             * of this matrix (EC_MI355X_JIT_SYNC=1: compiled at first call) */
+            ecd_combine_desc_t *d = new ecd_combine_desc_t;
+            memset(d, 0, sizeof(*d));
+            d->k = K;
+            d->rows = K;
+            d->nstripes = nst;
+            d->in_stride = ECD_CHUNK;
+            d->out_stride = (uint64_t)K * ECD_CHUNK;
+            for (int p = 0; p < K; ++p) {
+                d->in_base[p] = fr[p];
+                d->pat[p] = (uint8_t)p;
+                d->out_base[p] = bufB + (uint64_t)p * ECD_CHUNK;
+            }
+            memcpy(d->pat + K, c, (size_t)K * K);
+            d->npatterns = 1;
+            d->pat_bytes = K + K * K;
+            v.push_back({"library JIT (hiprtc)", bytes, [=](hipStream_t st) {
+                             ecj_lds_pad_kb = 0;
+                             if (ecdk_combine(st, d))
+                                 exit(9);
+                         }, bufB, ob});
+            /* 4 blocks per CU (8 waves) as the kb3 kernel's 204 VGPRs allow,
+             * instead of the 5 its 32 KiB tile allows */
+            v.push_back({"library JIT, 40 KiB LDS (4 blocks/CU)", bytes, [=](hipStream_t st) {
+                             ecj_lds_pad_kb = 8;
+                             if (ecdk_combine(st, d))
+                                 exit(9);
+                             ecj_lds_pad_kb = 0;
+                         }, bufB, ob});
+            v.push_back({"library JIT, 54 KiB LDS (2 blocks/CU)", bytes, [=](hipStream_t st) {
+                             ecj_lds_pad_kb = 22;
+                             if (ecdk_combine(st, d))
+                                 exit(9);
+                             ecj_lds_pad_kb = 0;
+                         }, bufB, ob});
+        }
+#endif
         add_combine_wm<1, 1>(v, "whole matrix 16 rows, compute only", a, bytes, bufB, ob);
         add_combine_wm<2, 1>(v, "whole matrix 2 x 8 rows, compute only", a, bytes, bufB, ob);
         {
@@ -1129,6 +1174,45 @@ int main(int argc, char **argv)
         }
         run_group("decode 16+4 dense, whole-matrix program (r06)", v, rounds, iters, s);
         v.clear();
+        /* the same with every fragment and the output in an allocation of its
+         * own, as torch tensors are (bench.py): placement moves multi-stream
+         * kernels */
+        static uint8_t *sep[17];
+        for (int p = 0; p < K; ++p) {
+            CHK(hipMalloc(&sep[p], nst * ECD_CHUNK));
+            CHK(hipMemcpy(sep[p], fr[p], nst * ECD_CHUNK, hipMemcpyDeviceToDevice));
+        }
+        CHK(hipMalloc(&sep[16], ob));
+        const CombineArgs *a2 = make_args(K, K, nst, sep, sep[16], true, c);
+        add_shipped_combine(v, "shipped, separate allocations", a2, bytes, sep[16], ob);
+        add_combine_wm<2, 0>(v, "whole matrix 2 x 8, separate allocations", a2, bytes, sep[16], ob);
+#ifdef KB3_WITH_JIT
+        {
+            ecd_combine_desc_t *d = new ecd_combine_desc_t;
+            memset(d, 0, sizeof(*d));
+            d->k = K;
+            d->rows = K;
+            d->nstripes = nst;
+            d->in_stride = ECD_CHUNK;
+            d->out_stride = (uint64_t)K * ECD_CHUNK;
+            for (int p = 0; p < K; ++p) {
+                d->in_base[p] = sep[p];
+                d->pat[p] = (uint8_t)p;
+                d->out_base[p] = sep[16] + (uint64_t)p * ECD_CHUNK;
+            }
+            memcpy(d->pat + K, c, (size_t)K * K);
+            d->npatterns = 1;
+            d->pat_bytes = K + K * K;
+            v.push_back({"library JIT, separate allocations", bytes, [=](hipStream_t st) {
+                             if (ecdk_combine(st, d))
+                                 exit(9);
+                         }, sep[16], ob});
+        }
+#endif
+        run_group("decode 16+4 dense, separate allocations (r06)", v, rounds, iters, s);
+        v.clear();
+        for (int p = 0; p < 17; ++p)
+            CHK(hipFree(sep[p]));
     }
     if (want(groups, "dec8"))
         decode_group(std::integral_constant<int, 8>{}, "decode 8+4 dense", false);
