@@ -125,8 +125,9 @@ struct Gen {
 };
 
 /* The program of output rows [r0, r1) over k inputs, as function prog<w>. */
-void emit_program(Gen &g, int w, u32 k, u32 rows_all, const uint8_t *coef, u32 r0, u32 r1)
+void emit_program(Gen &g, int w, u32 k, u32 T, const uint8_t *coef, u32 r0, u32 r1)
 {
+    const u32 ps = T * 64u;             /* plane stride of the tile */
     const u32 no = (r1 - r0) * 8;
     g.line("__device__ __forceinline__ void prog%d(u32 col, u32 *acc)", w);
     g.line("{");
@@ -142,13 +143,13 @@ void emit_program(Gen &g, int w, u32 k, u32 rows_all, const uint8_t *coef, u32 r
         decl += ", a" + std::to_string(o);
     g.line("%s;", decl.c_str());
     for (int b = 0; b < 8; ++b)
-        g.line("    n%d = LDW(col + %uu);", b, (u32)b * 256u);
+        g.line("    n%d = LDW(col + %uu);", b, (u32)b * ps);
     std::vector<bool> started(no, false);
     for (u32 p = 0; p < k; ++p) {
         g.line("    x0 = n0; x1 = n1; x2 = n2; x3 = n3; x4 = n4; x5 = n5; x6 = n6; x7 = n7;");
         if (p + 1 < k)
             for (int b = 0; b < 8; ++b)
-                g.line("    n%d = LDW(col + %uu);", b, ((p + 1) * 8 + (u32)b) * 256u);
+                g.line("    n%d = LDW(col + %uu);", b, ((p + 1) * 8 + (u32)b) * ps);
         g.line("    __builtin_amdgcn_sched_barrier(0);");
         g.line("    {");
         std::vector<u32> masks(no);
@@ -216,7 +217,6 @@ void emit_program(Gen &g, int w, u32 k, u32 rows_all, const uint8_t *coef, u32 r
     for (u32 o = 0; o < no; ++o)
         g.line("    acc[%u] = %s;", o, started[o] ? ("a" + std::to_string(o)).c_str() : "0u");
     g.line("}");
-    (void)rows_all;
 }
 
 const char *kPrologue = R"(
@@ -243,14 +243,17 @@ template <int LA>
 __device__ __forceinline__ void body(const JitArgs &a)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr u32 NW = T / 2u, PER = T / 2u, NT = NW * 64u;
     const u32 tid = threadIdx.x, lane = tid & 63u;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const u64 t0 = (u64)blockIdx.x * 4u;
-    for (u32 ins = wave; ins < K * 2u; ins += 2u) {
-        const u32 p = ins >> 1, el = (ins & 1u) * 64u + lane, seg = el >> 2;
-        const u64 st = t0 + (seg & 3u);
+    const u64 t0 = (u64)blockIdx.x * T;
+    /* the shipped tile kernels' staging (ec_kernels_impl.h stage_tile): input
+     * p, plane b, stripe s at ((p * 8 + b) * T + s) * 64 */
+    for (u32 ins = wave; ins < K * PER; ins += NW) {
+        const u32 p = ins / PER, el = (ins % PER) * 64u + lane, seg = el >> 2;
+        const u64 st = t0 + seg % T;
         if (st < a.nstripes) {
-            const unsigned char *gp = a.in[p] + st * a.in_stride + (seg >> 2) * 64u + (el & 3u) * 16u;
+            const unsigned char *gp = a.in[p] + st * a.in_stride + (seg / T) * 64u + (el & 3u) * 16u;
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)gp,
                                              (__attribute__((address_space(3))) void *)(lds + ins * 1024u),
                                              16, 0, LA);
@@ -261,43 +264,44 @@ __device__ __forceinline__ void body(const JitArgs &a)
      * build adds vmcnt(0) itself), so the wait is explicit */
     __builtin_amdgcn_s_waitcnt(0x0070);          /* vmcnt(0) lgkmcnt(0) */
     __syncthreads();
-    const u32 cs = lane >> 4, cc = lane & 15u;
-    const u32 col = (u32)(unsigned long long)(lds + cs * 64u + cc * 4u);
+    /* wave w: rows half (w & 1), stripes 4 * (w >> 1) .. + 3 */
+    const u32 half = wave & 1u, s = (wave >> 1) * 4u + (lane >> 4), cc = lane & 15u;
+    const u32 col = (u32)(unsigned long long)(lds + s * 64u + cc * 4u);
     u32 acc[NA];
-    if (wave == 0)
+    if (half == 0)
         prog0(col, acc);
     else
         prog1(col, acc);
     __syncthreads();
     /* stripe s, row r at (s * ROWS + r) * 512: a full decode's tile is then
      * its output as it lies in memory (ec_method_decode's stripe-major out) */
-    unsigned char *ob = lds + cs * (ROWS * 512u) + cc * 4u;
-    const u32 rb = wave == 0 ? 0u : R0;
-    const u32 nr = wave == 0 ? R0 : ROWS - R0;
+    unsigned char *ob = lds + s * (ROWS * 512u) + cc * 4u;
+    const u32 rb = half == 0 ? 0u : R0;
+    const u32 nr = half == 0 ? R0 : ROWS - R0;
 #pragma unroll
     for (u32 o = 0; o < NA; ++o)
         if (o < nr * 8u)
             *(u32 *)(ob + (rb + o / 8u) * 512u + (o % 8u) * 64u) = acc[o];
     __syncthreads();
     const u64 left = a.nstripes - t0;
-    const u32 ns = (u32)(left < 4u ? left : 4u);
+    const u32 ns = (u32)(left < T ? left : T);
     if (a.contig) {
-        /* one run of ns * ROWS * 512 bytes: 2 KiB per block instruction */
+        /* one run of ns * ROWS * 512 bytes */
         unsigned char *o = a.out[0] + t0 * a.out_stride;
-        for (u32 i = tid * 16u; i < ns * ROWS * 512u; i += 128u * 16u)
+        for (u32 i = tid * 16u; i < ns * ROWS * 512u; i += NT * 16u)
             __builtin_nontemporal_store(*(const v4u *)(lds + i), (v4u *)(o + i));
     } else {
         /* row by row: 512-byte runs, one per stripe (fragment-major outputs) */
         for (u32 r = 0; r < ROWS; ++r) {
-            const u32 s = tid >> 5, q = tid & 31u;
-            if (s < ns)
-                __builtin_nontemporal_store(*(const v4u *)(lds + (s * ROWS + r) * 512u + q * 16u),
-                                            (v4u *)(a.out[r] + (t0 + s) * a.out_stride + q * 16u));
+            const u32 ss = tid >> 5, q = tid & 31u;
+            if (ss < ns)
+                __builtin_nontemporal_store(*(const v4u *)(lds + (ss * ROWS + r) * 512u + q * 16u),
+                                            (v4u *)(a.out[r] + (t0 + ss) * a.out_stride + q * 16u));
         }
     }
 }
-extern "C" __global__ __launch_bounds__(128) void ec_jit_combine(JitArgs a) { body<0>(a); }
-extern "C" __global__ __launch_bounds__(128) void ec_jit_combine_nt(JitArgs a) { body<2>(a); }
+extern "C" __global__ __launch_bounds__(T / 2 * 64) void ec_jit_combine(JitArgs a) { body<0>(a); }
+extern "C" __global__ __launch_bounds__(T / 2 * 64) void ec_jit_combine_nt(JitArgs a) { body<2>(a); }
 )";
 
 /* ------------------------------------------------------------- hiprtc */
@@ -407,6 +411,16 @@ bool jit_sync()
     return v;
 }
 
+/* stripes per tile: 4 (two waves, 32 KiB of LDS for k = 16; up to 5 blocks
+ * per CU).  The body also takes 8 (four waves, 64 KiB, 2 blocks per CU, as
+ * the shipped k = 16 combine): 1-2 % slower through bench.py
+ * (profiles/r06/r06h_jitab.log), so 4. */
+constexpr u32 kJitTile = 4;
+u32 jit_tile()
+{
+    return kJitTile;
+}
+
 uint64_t jit_min_stripes()
 {
     static const uint64_t v = (uint64_t)env_long("EC_MI355X_JIT_MIN_STRIPES", 1024);
@@ -422,9 +436,10 @@ std::string source_of(const Key &key, u32 *ops)
     g.line("#define ROWS %uu", key.rows);
     g.line("#define R0 %uu", r0);
     g.line("#define NA %uu", r0 * 8);
+    g.line("#define T %uu", jit_tile());
 
-    emit_program(g, 0, key.k, key.rows, key.coef, 0, r0);
-    emit_program(g, 1, key.k, key.rows, key.coef, r0, key.rows);
+    emit_program(g, 0, key.k, jit_tile(), key.coef, 0, r0);
+    emit_program(g, 1, key.k, jit_tile(), key.coef, r0, key.rows);
     g.s += kBody;
     if (ops)
         *ops = g.ops;
@@ -620,11 +635,14 @@ extern "C" int ecj_launch(hipStream_t s, const ecd_combine_desc_t *d, int nt)
     a.contig = d->out_stride == (uint64_t)d->rows * 512;
     for (uint32_t r = 1; r < d->rows && a.contig; ++r)
         a.contig = a.out[r] == a.out[0] + (size_t)r * 512;
-    const size_t lds = (size_t)(d->k > d->rows ? d->k : d->rows) * 4 * 512 +
+    const u32 T = jit_tile();
+    const size_t lds = (size_t)(d->k > d->rows ? d->k : d->rows) * T * 512 +
                        (size_t)ecj_lds_pad_kb * 1024;
+    if (lds > (64u << 10))
+        return -EAGAIN;         /* the default dynamic LDS limit of a launch */
     void *params[] = {&a};
-    const hipError_t rc = hipModuleLaunchKernel(f, (u32)((d->nstripes + 3) / 4), 1, 1, 128, 1, 1,
-                                                (u32)lds, s, params, nullptr);
+    const hipError_t rc = hipModuleLaunchKernel(f, (u32)((d->nstripes + T - 1) / T), 1, 1, T / 2 * 64,
+                                                1, 1, (u32)lds, s, params, nullptr);
     if (rc != hipSuccess) {
         (void)hipGetLastError();
         return -EAGAIN;       /* the shipped kernel codes the call */
