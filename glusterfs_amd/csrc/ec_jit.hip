@@ -44,6 +44,7 @@
 #include <hip/hip_runtime.h>
 
 #include <dlfcn.h>
+#include <pthread.h>
 #include <errno.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -56,6 +57,7 @@
 #include <condition_variable>
 #include <deque>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -485,6 +487,13 @@ void compile_entry(Entry *e)
     e->state.store(st, std::memory_order_release);
 }
 
+/* The compile thread.  At exit it is stopped and joined (a compile in
+ * progress, <= ~2 s, finishes first): exit() runs the compiler's static
+ * destructors, and a compile still running in another thread would crash
+ * the process on its way out.  Queued matrices are dropped. */
+std::thread *g_worker;
+bool g_stop;
+
 void worker_main()
 {
     Jit &j = jit();
@@ -492,12 +501,51 @@ void worker_main()
         Entry *e;
         {
             std::unique_lock<std::mutex> g(j.mu);
-            j.cv.wait(g, [&] { return !j.queue.empty(); });
+            j.cv.wait(g, [&] { return g_stop || !j.queue.empty(); });
+            if (g_stop)
+                return;
             e = j.queue.front();
             j.queue.pop_front();
         }
         compile_entry(e);
     }
+}
+
+void worker_stop()
+{
+    Jit &j = jit();
+    {
+        std::lock_guard<std::mutex> g(j.mu);
+        g_stop = true;
+        j.queue.clear();
+    }
+    j.cv.notify_all();
+    if (g_worker && g_worker->joinable())
+        g_worker->join();
+}
+
+/* A child forked after the worker started has no worker (and maybe a held
+ * lock): it starts empty-queued, and its first queued matrix starts its own
+ * thread.  Entries the parent had queued stay "queued" in the child and
+ * keep running the shipped kernel. */
+void fork_prepare()
+{
+    jit().mu.lock();
+}
+
+void fork_parent()
+{
+    jit().mu.unlock();
+}
+
+void fork_child()
+{
+    Jit &j = jit();
+    new (&j.mu) std::mutex();
+    new (&j.cv) std::condition_variable();
+    j.queue.clear();
+    j.worker = false;
+    g_worker = nullptr;       /* the parent's thread object is not ours */
 }
 
 /* the entry of `key`, inserted (and queued or compiled) on first sight;
@@ -536,7 +584,12 @@ Entry *lookup(const Key &key)
         if (!jit_sync()) {
             j.queue.push_back(fresh);
             if (!j.worker) {
-                std::thread(worker_main).detach();
+                static std::once_flag once;
+                std::call_once(once, [] {
+                    atexit(worker_stop);
+                    pthread_atfork(fork_prepare, fork_parent, fork_child);
+                });
+                g_worker = new std::thread(worker_main);
                 j.worker = true;
             }
             j.cv.notify_one();

@@ -13,6 +13,7 @@ matrix once the code exists.  Every result is compared with the oracle:
   * the default asynchronous mode: the first call of a matrix runs the
     shipped kernel while a library thread compiles, later calls the
     compiled one -- exact both ways;
+  * a process exiting while its matrix compiles exits cleanly;
   * EC_MI355X_JIT=0: never compiled, never launched.
 Each case runs in its own process through the C ABI (the settings are read
 once per process)."""
@@ -129,6 +130,15 @@ assert s["launches"] >= 15 and s["failed"] == 0, s
 print("ok", s)
 """
 
+# a process that exits while its matrix is still being compiled: the compile
+# thread is joined at exit (a compile running through the compiler's static
+# destructors would crash the exit)
+EXIT = COMMON + r"""
+with g.ECMatrixList(16, 20) as L:
+    decode_check(L, 16, 20, 2048, 0xFFFF0)
+print("ok", g.jit_stats())
+"""
+
 OFF = COMMON + r"""
 with g.ECMatrixList(16, 20) as L:
     for _ in range(2):
@@ -158,6 +168,10 @@ def test_jit_full_size_round_trip():
 
 def test_jit_async_first_call_shipped_then_compiled():
     print(_run(ASYNC))
+
+
+def test_jit_exit_while_compiling():
+    print(_run(EXIT))
 
 
 def test_jit_off():
