@@ -17,6 +17,7 @@ from .ec_method import (  # noqa: F401
     gf_mul,
     host_registered,
     jit_compile_check,
+    jit_prepare,
     jit_stats,
     inject_device_faults,
     inverse_matrix,

@@ -170,6 +170,8 @@ void ecd_jit_stats(ecd_jit_stats_t *s);
  * output on failure. */
 int ecd_jit_compile_check(uint32_t k, uint32_t rows, const uint8_t *coef, uint32_t *ops,
                           char *log, size_t log_len);
+/* queue (or, EC_MI355X_JIT_SYNC=1, compile now) the kernel of a matrix */
+int ecd_jit_prepare(uint32_t k, uint32_t rows, const uint8_t *coef);
 
 #ifdef __cplusplus
 }

@@ -34,16 +34,21 @@
  *
  * Life of a pattern: a device combine with one pattern, k >= 12 and enough
  * stripes (EC_MI355X_JIT_MIN_STRIPES, default 1024) looks its coefficient
- * matrix up here.  The first sight queues a compile (hiprtc, ~1-2 s, on one
- * library thread) and the call runs the shipped kernel; once the code object
- * exists, calls of that matrix load it on their device (once) and launch it.
- * 32 matrices are kept, least recently used first out.  hiprtc is opened
- * with dlopen: without it (or with EC_MI355X_JIT=0) nothing changes.
- * EC_MI355X_JIT_SYNC=1 compiles on the calling thread (tests, benchmarks).
+ * matrix up here.  The first sight queues a compile (~1-2 s: the compiler
+ * process ec_jitc runs hiprtc, waited for by one library thread) and the call
+ * runs the shipped kernel; once the code object exists, calls of that matrix
+ * load it on their device (once) and launch it.  32 matrices are kept, least
+ * recently used first out.  Without ec_jitc or hiprtc (or with
+ * EC_MI355X_JIT=0) nothing changes.  EC_MI355X_JIT_SYNC=1 compiles on the
+ * calling thread (tests, benchmarks).
  */
 #include <hip/hip_runtime.h>
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
 #include <pthread.h>
 #include <errno.h>
 #include <stdarg.h>
@@ -64,6 +69,8 @@
 
 #include "ec_device.h"
 #include "ec_jit.h"
+
+extern char **environ;
 
 namespace {
 
@@ -306,52 +313,108 @@ extern "C" __global__ __launch_bounds__(T / 2 * 64) void ec_jit_combine(JitArgs 
 extern "C" __global__ __launch_bounds__(T / 2 * 64) void ec_jit_combine_nt(JitArgs a) { body<2>(a); }
 )";
 
-/* ------------------------------------------------------------- hiprtc */
+/* ----------------------------------------------------------- compiler */
 
-struct Rtc {
-    typedef int (*create_t)(void **, const char *, const char *, int, const char *const *,
-                            const char *const *);
-    typedef int (*compile_t)(void *, int, const char *const *);
-    typedef int (*size_t_fn)(void *, size_t *);
-    typedef int (*get_t)(void *, char *);
-    typedef int (*destroy_t)(void **);
-    create_t create = nullptr;
-    compile_t compile = nullptr;
-    size_t_fn log_size = nullptr, code_size = nullptr;
-    get_t log = nullptr, code = nullptr;
-    destroy_t destroy = nullptr;
+/* The compiler runs as a child process (ec_jitc, next to this library:
+ * hiprtc in a process of its own).  Round 6's first version called hiprtc on
+ * a library thread: a client that exited while that thread compiled crashed
+ * (the compiler's static destructors ran under the compile; reproduced on
+ * the CPU host with ec_method_jit_prepare + exit, 3 of 3 runs), and LLVM
+ * lived in every client's address space. */
+struct Compiler {
+    std::string path, why;
     bool ok = false;
-    std::string why;
 
-    Rtc()
+    Compiler()
     {
-        /* the loader's path first (a process that already mapped a hiprtc,
-         * e.g. torch's, gets that one), then the ROCm install */
-        void *h = nullptr;
-        for (const char *n : {"libhiprtc.so.7", "libhiprtc.so", "/opt/rocm/lib/libhiprtc.so.7"})
-            if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL)))
-                break;
-        if (!h) {
-            why = "libhiprtc not found";
-            return;
+        if (const char *e = getenv("EC_MI355X_JITC")) {
+            path = e;
+        } else {
+            Dl_info di;
+            if (dladdr((const void *)&ecd_jit_stats, &di) && di.dli_fname) {
+                path = di.dli_fname;
+                const size_t sl = path.rfind('/');
+                path = (sl == std::string::npos ? std::string(".") : path.substr(0, sl)) +
+                       "/ec_jitc";
+            }
         }
-        create = (create_t)dlsym(h, "hiprtcCreateProgram");
-        compile = (compile_t)dlsym(h, "hiprtcCompileProgram");
-        log_size = (size_t_fn)dlsym(h, "hiprtcGetProgramLogSize");
-        log = (get_t)dlsym(h, "hiprtcGetProgramLog");
-        code_size = (size_t_fn)dlsym(h, "hiprtcGetCodeSize");
-        code = (get_t)dlsym(h, "hiprtcGetCode");
-        destroy = (destroy_t)dlsym(h, "hiprtcDestroyProgram");
-        ok = create && compile && log_size && log && code_size && code && destroy;
+        ok = !path.empty() && access(path.c_str(), X_OK) == 0;
         if (!ok)
-            why = "libhiprtc lacks an entry point";
+            why = "compiler " + (path.empty() ? std::string("ec_jitc") : path) + " not found";
     }
 };
 
-Rtc &rtc()
+Compiler &compiler()
 {
-    static Rtc r;
-    return r;
+    static Compiler *c = new Compiler;   /* never destroyed (threads may outlive exit) */
+    return *c;
+}
+
+bool read_file(const std::string &p, std::vector<char> &out)
+{
+    FILE *f = fopen(p.c_str(), "rb");
+    if (!f)
+        return false;
+    char buf[1 << 16];
+    size_t n;
+    out.clear();
+    while ((n = fread(buf, 1, sizeof buf, f)) > 0)
+        out.insert(out.end(), buf, buf + n);
+    fclose(f);
+    return true;
+}
+
+/* 0: `code` holds the code object of `src`; else the compiler's log */
+int run_compiler(const std::string &src, std::vector<char> &code, std::string &log)
+{
+    Compiler &c = compiler();
+    if (!c.ok) {
+        log = c.why;
+        return -ENOSYS;
+    }
+    const char *tmp = getenv("TMPDIR");
+    std::string base = std::string(tmp && *tmp ? tmp : "/tmp") + "/ec_jit_XXXXXX";
+    std::vector<char> name(base.begin(), base.end());
+    name.push_back('\0');
+    const int fd = mkstemp(name.data());
+    if (fd < 0) {
+        log = "mkstemp failed";
+        return -EIO;
+    }
+    const std::string sp(name.data()), cp = sp + ".co", lp = sp + ".log";
+    const bool wrote = write(fd, src.data(), src.size()) == (ssize_t)src.size();
+    close(fd);
+    int rc = -EIO;
+    if (wrote) {
+        posix_spawn_file_actions_t fa;
+        posix_spawn_file_actions_init(&fa);
+        posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);
+        posix_spawn_file_actions_addopen(&fa, 2, lp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+        char *argv[] = {const_cast<char *>(c.path.c_str()), const_cast<char *>(sp.c_str()),
+                        const_cast<char *>(cp.c_str()), nullptr};
+        pid_t pid = -1;
+        if (posix_spawn(&pid, c.path.c_str(), &fa, nullptr, argv, environ) == 0) {
+            int st = 0;
+            while (waitpid(pid, &st, 0) < 0 && errno == EINTR) {
+            }
+            if (WIFEXITED(st) && WEXITSTATUS(st) == 0 && read_file(cp, code) && !code.empty())
+                rc = 0;
+            else
+                rc = WIFEXITED(st) && WEXITSTATUS(st) == 2 ? -ENOSYS : -EIO;
+        } else {
+            log = "posix_spawn of the compiler failed";
+        }
+        posix_spawn_file_actions_destroy(&fa);
+        if (rc) {
+            std::vector<char> l;
+            if (read_file(lp, l))
+                log += std::string(l.begin(), l.end());
+        }
+    }
+    unlink(sp.c_str());
+    unlink(cp.c_str());
+    unlink(lp.c_str());
+    return rc;
 }
 
 /* ------------------------------------------------------------- cache */
@@ -451,32 +514,12 @@ std::string source_of(const Key &key, u32 *ops)
 /* compile one entry (any thread; the result is published by `state`) */
 void compile_entry(Entry *e)
 {
-    Rtc &r = rtc();
     Jit &j = jit();
     const auto t0 = std::chrono::steady_clock::now();
     u32 ops = 0;
     const std::string src = source_of(e->key, &ops);
-    void *prog = nullptr;
-    int st = kFailed;
     std::string log;
-    if (r.ok && r.create(&prog, src.c_str(), "ec_jit.hip", 0, nullptr, nullptr) == 0) {
-        const char *opts[] = {"--offload-arch=gfx950", "-O3"};
-        const int rc = r.compile(prog, 2, opts);
-        size_t n = 0;
-        if (r.log_size(prog, &n) == 0 && n > 1) {
-            log.resize(n);
-            r.log(prog, &log[0]);
-        }
-        size_t cs = 0;
-        if (rc == 0 && r.code_size(prog, &cs) == 0 && cs > 0) {
-            e->code.resize(cs);
-            if (r.code(prog, e->code.data()) == 0)
-                st = kReady;
-        }
-        r.destroy(&prog);
-    } else {
-        log = r.ok ? "hiprtcCreateProgram failed" : r.why;
-    }
+    const int st = run_compiler(src, e->code, log) == 0 ? kReady : kFailed;
     j.compile_us += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
                         std::chrono::steady_clock::now() - t0).count();
     (st == kReady ? j.compiled : j.failed)++;
@@ -487,10 +530,10 @@ void compile_entry(Entry *e)
     e->state.store(st, std::memory_order_release);
 }
 
-/* The compile thread.  At exit it is stopped and joined (a compile in
- * progress, <= ~2 s, finishes first): exit() runs the compiler's static
- * destructors, and a compile still running in another thread would crash
- * the process on its way out.  Queued matrices are dropped. */
+/* The compile thread: it waits for the compiler process of each queued
+ * matrix.  It is neither stopped nor joined at exit (a compile then finishes
+ * in its own process, or is orphaned; nothing in this process is torn down
+ * under it: the cache and the compiler record are never destroyed). */
 std::thread *g_worker;
 bool g_stop;
 
@@ -509,19 +552,6 @@ void worker_main()
         }
         compile_entry(e);
     }
-}
-
-void worker_stop()
-{
-    Jit &j = jit();
-    {
-        std::lock_guard<std::mutex> g(j.mu);
-        g_stop = true;
-        j.queue.clear();
-    }
-    j.cv.notify_all();
-    if (g_worker && g_worker->joinable())
-        g_worker->join();
 }
 
 /* A child forked after the worker started has no worker (and maybe a held
@@ -585,10 +615,7 @@ Entry *lookup(const Key &key)
             j.queue.push_back(fresh);
             if (!j.worker) {
                 static std::once_flag once;
-                std::call_once(once, [] {
-                    atexit(worker_stop);
-                    pthread_atfork(fork_prepare, fork_parent, fork_child);
-                });
+                std::call_once(once, [] { pthread_atfork(fork_prepare, fork_parent, fork_child); });
                 g_worker = new std::thread(worker_main);
                 j.worker = true;
             }
@@ -659,7 +686,7 @@ extern "C" int ecj_eligible(const ecd_combine_desc_t *d)
 
 extern "C" int ecj_launch(hipStream_t s, const ecd_combine_desc_t *d, int nt)
 {
-    if (!ecj_eligible(d) || !rtc().ok)
+    if (!ecj_eligible(d) || !compiler().ok)
         return -EAGAIN;
     const uint8_t *pat = d->pat_ext ? d->pat_ext : d->pat;
     Key key;
@@ -716,14 +743,29 @@ extern "C" void ecd_jit_stats(ecd_jit_stats_t *st)
     st->entries = j.entries.size();
 }
 
+extern "C" int ecd_jit_prepare(uint32_t k, uint32_t rows, const uint8_t *coef)
+{
+    if (k < 1 || k > ECJ_MAX || rows < 2 || rows > ECJ_MAX || !coef)
+        return -EINVAL;
+    if (!jit_on())
+        return -EPERM;
+    if (!compiler().ok)
+        return -ENOSYS;
+    Key key;
+    key.k = k;
+    key.rows = rows;
+    memcpy(key.coef, coef, (size_t)k * rows);
+    return lookup(key) ? 0 : -ENOSPC;
+}
+
 extern "C" int ecd_jit_compile_check(uint32_t k, uint32_t rows, const uint8_t *coef, uint32_t *ops,
                                  char *log, size_t log_len)
 {
     if (k < 1 || k > ECJ_MAX || rows < 2 || rows > ECJ_MAX || !coef)
         return -EINVAL;
-    if (!rtc().ok) {
+    if (!compiler().ok) {
         if (log && log_len)
-            snprintf(log, log_len, "%s", rtc().why.c_str());
+            snprintf(log, log_len, "%s", compiler().why.c_str());
         return -ENOSYS;
     }
     Entry e;

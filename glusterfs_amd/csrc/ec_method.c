@@ -1501,6 +1501,12 @@ ec_method_jit_stats(ec_method_jit_stats_t *st)
 }
 
 int32_t
+ec_method_jit_prepare(uint32_t k, uint32_t rows, const uint8_t *coef)
+{
+    return ecd_jit_prepare(k, rows, coef);
+}
+
+int32_t
 ec_method_jit_compile_check(uint32_t k, uint32_t rows, const uint8_t *coef, uint32_t *ops)
 {
     char log[512];

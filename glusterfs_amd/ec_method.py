@@ -44,7 +44,7 @@ EXPORTS = (
     "ec_method_inject_device_faults", "ec_method_device_numa_node", "ec_method_copy_threads",
     "ec_method_host_register_async", "ec_method_host_register_flush", "ec_method_buffer_get",
     "ec_method_buffer_put", "ec_method_pool_stats", "ec_method_jit_stats",
-    "ec_method_jit_compile_check", "ec_method_xover_route",
+    "ec_method_jit_compile_check", "ec_method_jit_prepare", "ec_method_xover_route",
     "ec_method_xover_split",
     "ec_method_xover_plan",
     "ec_method_xover_observe_split",
@@ -175,6 +175,7 @@ def _load():
         "ec_method_pool_stats": (None, [ctypes.POINTER(PoolStats)]),
         "ec_method_jit_stats": (None, [ctypes.POINTER(JitStats)]),
         "ec_method_jit_compile_check": (i32, [u32, u32, vp, ctypes.POINTER(u32)]),
+        "ec_method_jit_prepare": (i32, [u32, u32, vp]),
         "ec_method_xover_route": (i32, [u32, i32, u64, u64, u64, u64]),
         "ec_method_xover_split": (i32, [u32, i32, u64, u64, u64, u64]),
         "ec_method_xover_plan": (i32, [u32, i32, u64, u64, u64, u64, u32, ctypes.POINTER(i32)]),
@@ -270,6 +271,13 @@ def jit_compile_check(k, rows, coef):
     ops = ctypes.c_uint32(0)
     rc = lib.ec_method_jit_compile_check(k, rows, c.ctypes.data, ctypes.byref(ops))
     return rc, ops.value
+
+
+def jit_prepare(k, rows, coef):
+    """Queue the kernel of a rows x k coefficient matrix for compilation."""
+    import numpy as np
+    c = np.ascontiguousarray(np.asarray(coef, dtype=np.uint8).reshape(rows, k))
+    return lib.ec_method_jit_prepare(k, rows, c.ctypes.data)
 
 
 def pool_stats():

@@ -433,6 +433,11 @@ typedef struct {
     uint64_t entries;     /* matrices in the cache now (<= 32)          */
 } ec_method_jit_stats_t;
 void ec_method_jit_stats(ec_method_jit_stats_t *stats);
+/* Queue the kernel of a rows x k coefficient matrix for compilation before
+ * its first call (e.g. a heal daemon that knows the bricks it will read):
+ * 0, -EPERM (EC_MI355X_JIT=0), -ENOSYS (no hiprtc), -ENOSPC (the per-process
+ * compile budget is spent), -EINVAL.  Needs no device. */
+int32_t ec_method_jit_prepare(uint32_t k, uint32_t rows, const uint8_t *coef);
 /* Generate and compile (without loading) the kernel of a rows x k matrix of
  * GF(2^8) coefficients (row-major): returns its code size in bytes, or
  * -errno (-ENOSYS without hiprtc, -EIO when the compiler failed); *ops, when

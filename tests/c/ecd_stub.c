@@ -121,3 +121,5 @@ int ecd_copy_threads(void) { return 0; }
 void ecd_jit_stats(ecd_jit_stats_t *s) { memset(s, 0, sizeof(*s)); }
 int ecd_jit_compile_check(uint32_t k, uint32_t r, const uint8_t *c, uint32_t *o, char *l, size_t n)
 { (void)k; (void)r; (void)c; (void)o; (void)l; (void)n; return -ENOSYS; }
+int ecd_jit_prepare(uint32_t k, uint32_t r, const uint8_t *c)
+{ (void)k; (void)r; (void)c; return -ENOSYS; }

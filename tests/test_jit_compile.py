@@ -47,3 +47,29 @@ def test_jit_compile_check_rejects_bad_geometry():
     import glusterfs_amd as g
     assert g.jit_compile_check(17, 16, np.ones(17 * 16, np.uint8))[0] == -22
     assert g.jit_compile_check(16, 1, np.ones(16, np.uint8))[0] == -22
+
+
+EXIT_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, %r)
+import glusterfs_amd as g
+rng = np.random.default_rng(int(sys.argv[1]))
+coef = rng.integers(1, 256, 256, dtype=np.uint8)       # a fresh matrix: no compiler cache hit
+assert g.jit_prepare(16, 16, coef) in (0, -38), "prepare"
+print("queued", flush=True)
+"""
+
+
+def test_exit_while_a_matrix_compiles():
+    """A client that exits while a matrix is still being compiled exits
+    cleanly (the compile runs in the ec_jitc process; round 6's first
+    version compiled on a library thread and crashed such exits in 3 of 3
+    runs).  Five processes, each exiting right after queueing."""
+    import subprocess
+    import sys
+    env = dict(os.environ, EC_MI355X_QUIET="1")
+    env.pop("EC_MI355X_JIT_SYNC", None)
+    for seed in range(5):
+        r = subprocess.run([sys.executable, "-c", EXIT_SCRIPT % ROOT, str(seed)], env=env,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "queued" in r.stdout, (r.returncode, r.stderr[-2000:])
