@@ -19,7 +19,7 @@ import json
 import os
 import sys
 
-OURS = ("ec_combine", "ec_encode_vander", "ec_encode_tile", "ec_slots")
+OURS = ("ec_jit_combine", "ec_combine", "ec_encode_vander", "ec_encode_tile", "ec_slots")
 
 
 def short(name):
