@@ -340,7 +340,8 @@ def main():
         L.fini()
     print(json.dumps(dict(seed=seed0, threads=nth, secs=secs, calls=counts,
                           gpu_calls=st["gpu_calls"], cpu_calls=st["cpu_calls"],
-                          cpu_fallbacks=st["cpu_fallbacks"], mismatches=bad[:5])), flush=True)
+                          cpu_fallbacks=st["cpu_fallbacks"], jit=g.jit_stats(),
+                          mismatches=bad[:5])), flush=True)
     return 1 if bad else 0
 
 

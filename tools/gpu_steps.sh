@@ -5,7 +5,7 @@
 # Steps: smoke | pytest | pytest_new (the files in $TESTS) | bench | bench_rocprof
 #        | rehearsal (2 gloo ranks on GPU 0) | profile (per-config rocprof + PMC)
 #        | kbench (tools/kbench/kbench $KBENCH_ARGS) | kb3 (tools/kbench/kb3 $KB3_ARGS)
-#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | zcheal (pinned 16+4 / 8+4 decode, encode, heal, row-masked encode, ZCDB A/B) | fuzz (tools/fuzz_api.py: random calls of every entry point and buffer kind against the oracle, GPU-always then auto) | pcie (DMA copy ceiling of the link, each way and duplex) | zctpb (pinned decodes + encodes 1-256 MiB by EC_ZC_TPB / EC_ZC_INFLIGHT_KB) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | ablib (tools/ab_lib.sh: two library builds alternating through bench.py --only) | concur (tools/kbench/concur: concurrent vs coalesced-ceiling calls, auto / gpu / cpu) | sharesweep (heal sweep, auto, split share fixed per mille; 0 = the model's) | busyab (heal windows on $BUSY_BUFS buffers from 2/4/8 threads, the busy-staging rule off / on, and CPU-only) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
+#        | zcab (heal sweep, zero-copy combine A/B) | zcsizes (pinned decodes 4-256 MiB, A/B) | zcheal (pinned 16+4 / 8+4 decode, encode, heal, row-masked encode, ZCDB A/B) | fuzz (tools/fuzz_api.py: random calls of every entry point and buffer kind against the oracle, GPU-always then auto) | fuzzjit (device buffers only, the run-time compiled kernels from 16 stripes up) | pcie (DMA copy ceiling of the link, each way and duplex) | zctpb (pinned decodes + encodes 1-256 MiB by EC_ZC_TPB / EC_ZC_INFLIGHT_KB) | hsweep (kernel trace of the 4 MiB heal sweep, GPU engine) | hostlat (host cost of one device call) | hsweep3 (heal sweep by buffer provenance, auto / gpu / cpu) | ablib (tools/ab_lib.sh: two library builds alternating through bench.py --only) | concur (tools/kbench/concur: concurrent vs coalesced-ceiling calls, auto / gpu / cpu) | sharesweep (heal sweep, auto, split share fixed per mille; 0 = the model's) | busyab (heal windows on $BUSY_BUFS buffers from 2/4/8 threads, the busy-staging rule off / on, and CPU-only) | trace (per-launch rocprof sequence, STEPS launches of $TRACE_ARGS)
 # Logs go to gpurun_out/${TAG}_<step>.log.
 set -u
 mkdir -p gpurun_out
@@ -36,6 +36,7 @@ for step in "$@"; do
     zctpb) run zctpb 900 bash -c 'for r in 1 2; do for c in "0 2048" "4 2048" "0 1024" "0 4096"; do set -- $c; EC_GPU_ALWAYS=1 EC_ZC_TPB=$1 EC_ZC_INFLIGHT_KB=$2 ZC_SIZES="${ZC_SIZES:-1 2 4 8 16 64 256}" python3 tools/zc_sizes.py || exit 1; done; done' ;;
     zcheal) run zcheal 600 bash -c 'for r in 1 2; do for v in 0 1; do EC_GPU_ALWAYS=1 EC_MI355X_ZCDB=$v ZC_GEOS="16+4 8+4" ZC_SIZES="4 16 64" python3 tools/zc_sizes.py || exit 1; done; done' ;;
     fuzz) run fuzz $(( ${FUZZ_SECS:-150} + 300 )) bash -c 'EC_GPU_ALWAYS=1 FUZZ_SECS=${FUZZ_SECS:-150} python3 -u tools/fuzz_api.py && EC_GPU_ALWAYS=0 FUZZ_SECS=60 python3 -u tools/fuzz_api.py' ;;
+    fuzzjit) run fuzzjit $(( ${FUZZ_SECS:-120} + 200 )) bash -c 'EC_GPU_ALWAYS=1 EC_MI355X_JIT_MIN_STRIPES=16 FUZZ_KINDS="device device_offset" FUZZ_SECS=${FUZZ_SECS:-120} python3 -u tools/fuzz_api.py' ;;
     rmwab) run rmwab 600 bash -c 'export EC_GPU_ALWAYS=1 FUZZ_THREADS=12 FUZZ_SECS=${FUZZ_SECS:-100} FUZZ_KINDS="device device_offset" FUZZ_OPS="writev decode encode stream_chain"; echo "== default (LDS-DMA at the caller alignment)"; python3 -u tools/fuzz_api.py; a=$?; echo "== EC_MI355X_ENC=0 (register encoders, aligned loads + alignbyte)"; EC_MI355X_ENC=0 python3 -u tools/fuzz_api.py; b=$?; echo "rc default=$a enc0=$b"' ;;
     regrepro) run regrepro 600 env EC_GPU_ALWAYS=1 python3 -u tools/reg_repro.py ${REPRO_ITERS:-60} ;;
     pcie) run pcie 200 bash -c 'for m in 4 16 256; do python3 tools/pcie_probe.py $m || exit 1; done' ;;
