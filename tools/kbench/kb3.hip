@@ -355,6 +355,82 @@ static void add_combine_wm(std::vector<Variant> &v, const char *nm, const Combin
                  }, MODE == 0 ? out : nullptr, ob});
 }
 
+/* r06: the run-time four-Russians combine (tools/gen/gen_fr_asm.py ->
+ * kb_fr16.h): the decode matrix is a run-time argument, as in the shipped
+ * kernel, but each wave runs 8 rows at once -- per input, the 22 XOR
+ * combinations of its two 4-plane groups are built once into registers and
+ * every row's multiply-accumulate is an 8-instruction body (a jump per row
+ * and input, GPR-indexed to the row's accumulators) instead of a 12.85-
+ * instruction program that re-reads the input's planes from LDS.  One
+ * 4-stripe tile per block, two waves (rows 0-7, 8-15).  w.cw[p * 4 + q]:
+ * the coefficients of input p for rows 4q .. 4q + 3, one byte each. */
+#include "kb_fr16.h"
+struct FRW {
+    u32 cw[64];
+};
+
+template <int LA>
+__global__ __launch_bounds__(128) void kb_combine_fr(const CombineArgs a, const FRW w)
+{
+    constexpr int T = 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const u32 tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * T;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 lane = tid & 63u;
+    stage_tile<T, 2, LA>(lds, [&](u32 p, uint64_t st) {
+        return a.in_base[p] + st * a.in_stride;
+    }, 16, t0, a.nstripes, wave, lane);
+    __syncthreads();
+    const u32 cs = lane >> 4, cc = lane & 15u;
+    const uint8_t *col = lds + cs * 64u + cc * 4u;
+    u32 acc[64];
+#pragma unroll
+    for (int o = 0; o < 64; ++o)
+        acc[o] = 0;
+#pragma unroll 1
+    for (u32 p = 0; p < 16; ++p) {
+        u32 x[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            x[b] = *reinterpret_cast<const u32 *>(col + (p * 8 + b) * (T * 64u));
+        const u32 cw0 = __builtin_amdgcn_readfirstlane(w.cw[p * 4 + wave * 2]);
+        const u32 cw1 = __builtin_amdgcn_readfirstlane(w.cw[p * 4 + wave * 2 + 1]);
+        FR_ASM_ROWS8(x, cw0, cw1, acc);
+    }
+    __syncthreads();
+    uint8_t *ob = lds + cs * 8192u + cc * 4u + wave * 4096u;
+#pragma unroll
+    for (int o = 0; o < 64; ++o)
+        *reinterpret_cast<u32 *>(ob + (o >> 3) * 512u + (o & 7) * 64u) = acc[o];
+    __syncthreads();
+    uint8_t *o = a.out_base[0] + t0 * a.out_stride;
+    const uint64_t left = a.nstripes - t0;
+    const u32 nbytes = (u32)(left < T ? left : T) * 8192u;
+    for (u32 i = tid * 16u; i < (u32)T * 8192u; i += 128u * 16u)
+        if (i < nbytes)
+            __builtin_nontemporal_store(*reinterpret_cast<const v4u *>(lds + i),
+                                        reinterpret_cast<v4u *>(o + i));
+}
+
+static void add_combine_fr(std::vector<Variant> &v, const char *nm, const CombineArgs *a,
+                           const uint8_t *coef, double bytes, uint8_t *out, size_t ob)
+{
+    FRW *w = new FRW;
+    memset(w, 0, sizeof(*w));
+    for (int p = 0; p < 16; ++p)
+        for (int r = 0; r < 16; ++r)
+            w->cw[p * 4 + r / 4] |= (u32)coef[r * 16 + p] << (8 * (r % 4));
+    const bool nt = nt_staging(a->nstripes * 16 * ECD_CHUNK);
+    const void *kern = nt ? (const void *)kb_combine_fr<kLdsDmaNT>
+                          : (const void *)kb_combine_fr<kLdsDmaDefault>;
+    const uint64_t g = (a->nstripes + 3) / 4;
+    v.push_back({nm, bytes, [=](hipStream_t st) {
+                     void *args[] = {(void *)a, (void *)w};
+                     CHK(hipLaunchKernel(kern, dim3((u32)g), dim3(128), args, 32u << 10, st));
+                 }, out, ob});
+}
+
 /* Double-buffered persistent combine for k = 16 (r03 candidate, measured slower: DESIGN.md 3.3.1).  The 8-stripe
  * tile of ec_combine is split into two 32 KiB halves (inputs 0-7, 8-15) that
  * stay within the 64 KiB of one block, so two blocks still share a CU, and
@@ -1162,6 +1238,7 @@ int main(int argc, char **argv)
                          }, bufB, ob});
         }
 #endif
+        add_combine_fr(v, "run-time four-Russians (8 rows per wave)", a, c, bytes, bufB, ob);
         add_combine_wm<1, 1>(v, "whole matrix 16 rows, compute only", a, bytes, bufB, ob);
         add_combine_wm<2, 1>(v, "whole matrix 2 x 8 rows, compute only", a, bytes, bufB, ob);
         {
