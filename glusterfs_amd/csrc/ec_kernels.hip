@@ -176,13 +176,8 @@ int launch_combine(hipStream_t s, const CombineArgs &a)
         return -EINVAL;
     const size_t lds = combine_lds<1>(a.k);
     if (a.patg) {
-        /* k = 16: 64 KiB tile + the pattern is past the 64 KiB default */
-        const void *kern = (const void *)ec_combine<K, 1, NW, true, NTS, 2, true, true, 1, SL, 1, LA>;
-        if (lds + kPatLdsBytes > (64u << 10) &&
-            ensure_lds_limit(kern, (int)(combine_lds<1>(K) + kPatLdsBytes)) != 0)
-            return -EIO;
         hipLaunchKernelGGL((ec_combine<K, 1, NW, true, NTS, 2, true, true, 1, SL, 1, LA>), dim3((u32)g),
-                           dim3(NW * 64), lds + kPatLdsBytes, s, a);
+                           dim3(NW * 64), lds, s, a);
     } else if (a.group_pattern) {
         hipLaunchKernelGGL((ec_combine<K, 1, NW, true, NTS, 2, false, true, 1, SL, 1, LA>), dim3((u32)g),
                            dim3(NW * 64), lds, s, a);
@@ -734,7 +729,7 @@ int launch_n1(hipStream_t s, const CombineArgs &a, uint64_t g)
         return 0;
     if (g > 0x7fffffffull)
         return -EINVAL;
-    const size_t lds = combine_n_lds<NW, WOT, PG>((int)a.k);
+    const size_t lds = combine_n_lds<NW, WOT>((int)a.k);
     hipLaunchKernelGGL((ec_combine_n<K, NW, MIXED, NTS, WOT, PG, SL, 1, LA>), dim3((u32)g),
                        dim3(NW * 64), lds, s, a);
     return launch_ok("launch_n1");

@@ -961,17 +961,6 @@ struct CombineArgs {
 
 constexpr u32 kMaxPatWords = 128; /* one pattern: kw * (1 + rows) <= 4 * 32 */
 
-/* The words of the block's pattern (src[] then one row of coefficients per
- * output).  PG = false: the kernel-argument segment, read by scalar loads.
- * PG = true (mixed calls with more patterns than the 2 KiB argument space
- * holds, e.g. > 7 erasure masks of a 16+4 volume): the pattern table in
- * device memory -- the per-call cache of decode matrices.  Each block loads
- * its pattern once (lane i: words i, i + 64) before any store is issued,
- * keeps the src[] words in SGPRs for staging and parks the rest in LDS after
- * the tile, where a coefficient word is one broadcast ds_read.  (A vector
- * load per coefficient would need a vmcnt(0) wait that also drains the
- * outstanding stores; keeping the words in VGPRs cost the k = 16 kernel its
- * second block per CU: 68 VGPRs.) */
 /* A wave-uniform dword of read-only global memory by a scalar load (constant
  * address space: s_load_dword through the scalar cache).  As a vector load
  * it was global_load + s_waitcnt vmcnt(0) at the head of every block, before
@@ -984,23 +973,33 @@ __device__ __forceinline__ u32 scalar_load_u32(const void *p)
     return *reinterpret_cast<const __attribute__((address_space(4))) u32 *>(a);
 }
 
+/* The words of the block's pattern (src[] then one row of coefficients per
+ * output).  PG = false: the kernel-argument segment, read by scalar loads.
+ * PG = true (mixed calls with more patterns than the 2 KiB argument space
+ * holds, e.g. > 7 erasure masks of a 16+4 volume): the pattern table in
+ * device memory -- the per-call cache of decode matrices -- read the same
+ * way, by scalar loads through the scalar cache: the src[] words once per
+ * block (the staging addresses need them first), a row's coefficient words
+ * when the row starts.
+ * (r04-r06 loaded the whole pattern by vector loads and parked it in LDS
+ * after the tile, a coefficient word then one broadcast ds_read: the k = 16
+ * kernel's tile grew past 64 KiB and every wave issued the pattern loads
+ * beside its staging, 3 % slower than the same patterns from the argument
+ * segment, profiles/r06/r06r_kb3_mixed.log.  A vector load per coefficient
+ * would need a vmcnt(0) wait that also drains the outstanding stores, and
+ * the words in VGPRs cost the k = 16 kernel its second block per CU.) */
 template <bool PG>
 struct PatWords {
     u32 pb;
     u32 s0, s1, s2, s3;          /* PG: the src[] words */
-    u32 v0, v1;                  /* PG: this lane's words of the pattern */
-    const u32 *lp;               /* PG: the pattern in LDS */
-    __device__ __forceinline__ PatWords(const CombineArgs &a, u32 pat, u32 lane, uint8_t *lds_pat)
+    const u32 *t;                /* PG: the pattern in the device table */
+    __device__ __forceinline__ PatWords(const CombineArgs &a, u32 pat)
     {
         pb = pat * a.pwords;
         if constexpr (PG) {
-            const u32 *t = a.patg + pb;
-            /* the src[] words by one scalar load (the staging addresses need
-             * them first; pwords >= 2 kw, so 4 words stay in the pattern
-             * when kw >= 2, 2 when kw = 1); the whole pattern by vector
-             * loads whose LDS copy park() writes after the staging is
-             * issued (r04: written here, the copy's vmcnt(0) held back the
-             * staging of every block) */
+            t = a.patg + pb;
+            /* the src[] words by one scalar load (pwords >= 2 kw, so 4 words
+             * stay in the pattern when kw >= 2, 2 when kw = 1) */
             if (a.kw >= 2) {
                 const v4u q = *reinterpret_cast<const __attribute__((address_space(4))) v4u *>(
                     (uintptr_t)t);
@@ -1014,21 +1013,6 @@ struct PatWords {
                 s0 = q.x;
                 s1 = s2 = s3 = 0u;
             }
-            v0 = lane < a.pwords ? t[lane] : 0u;
-            v1 = lane + 64u < a.pwords ? t[lane + 64u] : 0u;
-            lp = reinterpret_cast<const u32 *>(lds_pat);
-        }
-    }
-    /* PG: the pattern into LDS (wave 0), after the staging has been issued;
-     * visible to every wave after the staging barrier */
-    __device__ __forceinline__ void park(u32 lane) const
-    {
-        if constexpr (PG) {
-            u32 *w = const_cast<u32 *>(lp);
-            if (threadIdx.x < 64u) {
-                w[lane] = v0;
-                w[lane + 64u] = v1;
-            }
         }
     }
     /* (the argument struct is passed in, not held: holding a reference to
@@ -1036,7 +1020,7 @@ struct PatWords {
     __device__ __forceinline__ u32 word(const CombineArgs &a, u32 rel) const
     {
         if constexpr (PG)
-            return __builtin_amdgcn_readfirstlane(lp[rel]);
+            return scalar_load_u32(t + rel);
         else
             return a.pat[pb + rel];
     }
@@ -1055,8 +1039,6 @@ struct PatWords {
         return __builtin_amdgcn_readfirstlane((w >> ((idx & 3u) * 8u)) & 0xFFu);
     }
 };
-
-constexpr size_t kPatLdsBytes = kMaxPatWords * 4; /* PG kernels: LDS after the tile */
 
 
 /* pattern id of the tile starting at stripe t0 (ids past the table clamp to
@@ -1193,7 +1175,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
     /* a sorted tile is one pattern's: take it from the tile's first stripe
      * (never padding: runs are padded at their end, to 8 slots) */
     const uint64_t tp = SLOTS ? slot_stripe<SLOTS>(a, t0, nslots) : t0;
-    const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp), lane, lds + k * (T * ECD_CHUNK));
+    const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp));
 
     /* stage: every wave instruction (global_load_lds_dwordx4) fills 1 KiB of
      * LDS linearly = planes b, b+1 of input p for the tile's 8 stripes (T=8)
@@ -1219,7 +1201,6 @@ __global__ __launch_bounds__(NW * 64) void ec_combine(const CombineArgs a)
                 (__attribute__((address_space(3))) void *)(lds + ins * 1024u), 16, 0, LA);
         }
     }
-    pw.park(lane);
     __syncthreads();
 
     /* compute: (row, 8-stripe subtile) items spread over the NW waves */
@@ -1308,14 +1289,12 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
     if (SLOTS && tp == kNoSlot)
         return;
     constexpr u32 SLICE = WOT ? (T / WOT) * ECD_CHUNK : 0;
-    /* LDS: the k-input tile, NW output slices, then (PG) the pattern */
-    const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp), lane,
-                          lds + k * T * ECD_CHUNK + NW * SLICE);
+    /* LDS: the k-input tile, then NW output slices */
+    const PatWords<PG> pw(a, tile_pattern<MIXED>(a, tp));
     stage_tile<T, NW, LA>(lds, [&](u32 p, uint64_t slot) -> const uint8_t * {
         const uint64_t st = slot_stripe<SLOTS>(a, slot, nslots);
         return st != kNoSlot ? a.in_base[pw.byte(a, p)] + st * a.in_stride : nullptr;
     }, k, t0, SLOTS ? (uint64_t)nslots : a.nstripes, wave, lane);
-    pw.park(lane);
     __syncthreads();
     const u32 cs = lane >> 4, cc = lane & 15u;
     const uint8_t *col = lds + cs * 64u + cc * 4u;
@@ -1393,11 +1372,10 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_n(const CombineArgs a)
 }
 
 /* dynamic LDS of an ec_combine_n launch for k inputs */
-template <int NW, int WOT, bool PG = false>
+template <int NW, int WOT>
 constexpr size_t combine_n_lds(int k)
 {
-    return (size_t)k * 4 * ECD_CHUNK + (WOT ? (size_t)NW * (4 / WOT) * ECD_CHUNK : 0) +
-           (PG ? kPatLdsBytes : 0);
+    return (size_t)k * 4 * ECD_CHUNK + (WOT ? (size_t)NW * (4 / WOT) * ECD_CHUNK : 0);
 }
 
 /* Zero-copy variant for the host-buffer path, where every input and output
@@ -1429,7 +1407,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc(const CombineArgs a)
     const u32 lane = tid & 63u;
     uint8_t *otile = lds + k * (T * ECD_CHUNK);
 
-    const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
+    const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0));
 
     /* stage: wave instruction ins = 1 KiB = stripes 2q, 2q+1 of input p */
     const u32 ni = k * (T / 2);
@@ -1567,7 +1545,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
      * 2q, 2q + 1 of input p (as ec_combine_zc) */
     auto stage = [&](uint64_t t, u32 b) {
         const uint64_t t0 = t * T;
-        const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
+        const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0));
         uint8_t *buf = lds + b * tb;
         const u32 ni = k * (T / 2);
         for (u32 ins = wave; ins < ni; ins += NW) {
@@ -1602,7 +1580,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_zc_db(const CombineArgs a)
         const uint64_t t0 = t * T;
         const uint8_t *buf = lds + (i & 1u) * tb;
         {
-            const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0), lane, nullptr);
+            const PatWords<false> pw(a, tile_pattern<MIXED>(a, t0));
             for (u32 r = wave; r < rows; r += NW) {
                 const uint8_t *col = buf + cs * ECD_CHUNK + cc * (4u * CW);
                 const u32 rw = a.kw * (1 + r);

@@ -461,7 +461,7 @@ __global__ __launch_bounds__(NW * 64) void ec_combine_db(const CombineArgs a)
     if (t >= ntiles)
         return;
     const uint64_t last = a.nstripes - 1;
-    const PatWords<false> pw(a, 0u, lane, nullptr);
+    const PatWords<false> pw(a, 0u);
     /* half h of tile `tile`: input p = 8h + ins / 4, 1 KiB per instruction */
     auto stage = [&](uint64_t tile, u32 h) {
 #pragma unroll
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(16 * 64) void ec_combine_pd(const CombineArgs a)
         return;
     const uint64_t last = a.nstripes - 1;
     auto stage = [&](uint64_t tile) {
-        const PatWords<false> pw(a, tile_pattern<MIX>(a, tile * T), lane, nullptr);
+        const PatWords<false> pw(a, tile_pattern<MIX>(a, tile * T));
 #pragma unroll
         for (u32 j = 0; j < 4; ++j) {
             const u32 ins = j * NW + wave;
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(16 * 64) void ec_combine_pd(const CombineArgs a)
         for (int b = 0; b < 8; ++b)
             acc[b][0] = acc[b][1] = 0;
         if (has) {
-            const PatWords<false> pw(a, tile_pattern<MIX>(a, t * T), lane, nullptr);
+            const PatWords<false> pw(a, tile_pattern<MIX>(a, t * T));
             const u32 rw = a.kw * (1 + r);
             uint64_t cl = (uint64_t)pw.word(a, rw) | ((uint64_t)pw.word(a, rw + 1) << 32);
             uint64_t ch = (uint64_t)pw.word(a, rw + 2) | ((uint64_t)pw.word(a, rw + 3) << 32);
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(16 * 64) void kb_combine_probe(const CombineArgs a)
     const uint64_t t0 = (uint64_t)blockIdx.x * T;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 lane = tid & 63u;
-    const PatWords<false> pw(a, 0u, lane, nullptr);
+    const PatWords<false> pw(a, 0u);
     if constexpr (!(MODE & 1)) {
 #pragma unroll
         for (u32 j = 0; j < NI / NW; ++j) {
@@ -1314,8 +1314,11 @@ int main(int argc, char **argv)
         run_group("decode 8+4, 64K stripes", v, rounds, iters, s);
         v.clear();
     }
-    auto mixed_group = [&](auto kk, int n, int np, const char *title) {
-        /* np random dense patterns over n fragments, 1024-stripe groups */
+    auto mixed_group = [&](auto kk, int n, int np, const char *title, bool spaced = false) {
+        /* np random dense patterns over n fragments, 1024-stripe groups.
+         * spaced (r06): fragment f at f * nst * 512 (disjoint, as the dense
+         * decode groups lay them), else at f * nst * 512 * K / n (overlapping:
+         * the pre-r06 layout, kept for comparison) */
         constexpr int K = decltype(kk)::value;
         const uint64_t nst = user / (K * ECD_CHUNK);
         ecd_combine_desc_t d;
@@ -1326,7 +1329,8 @@ int main(int argc, char **argv)
         d.in_stride = ECD_CHUNK;
         d.out_stride = (uint64_t)K * ECD_CHUNK;
         for (int f = 0; f < n; ++f)
-            d.in_base[f] = bufA + (uint64_t)f * nst * ECD_CHUNK * K / n;
+            d.in_base[f] = bufA + (spaced ? (uint64_t)f * nst * ECD_CHUNK
+                                          : (uint64_t)f * nst * ECD_CHUNK * K / n);
         for (int r = 0; r < K; ++r)
             d.out_base[r] = bufB + (uint64_t)r * ECD_CHUNK;
         d.npatterns = np;
@@ -1359,13 +1363,82 @@ int main(int argc, char **argv)
         d.group_pattern = dgp;
         d.group_shift = 10;
         CombineArgs *a = new CombineArgs;
-        if (ecdk_pack_args(&d, a) != 0) {
-            printf("(%s: pattern table case not covered here)\n", title);
-            return;
-        }
         const double bytes = 2.0 * nst * K * ECD_CHUNK;
         const size_t ob = (size_t)nst * K * ECD_CHUNK;
+        {
+            /* the library's device entry: packs, uploads the pattern table
+             * when the patterns exceed the argument space (bench's 64-mask
+             * 16+4 call), launches */
+            ecd_combine_desc_t *dl = new ecd_combine_desc_t(d);
+            v.push_back({"library (ecdk_combine)", bytes, [=](hipStream_t st) {
+                             if (ecdk_combine(st, dl))
+                                 exit(9);
+                         }, bufB, ob});
+        }
+        if (ecdk_pack_args(&d, a) != 0) {
+            /* the device-table case: the library variant, and the same
+             * kernel with the table uploaded once (no per-call host work) */
+            std::vector<u32> w((size_t)a->pwords * a->npatterns, 0u);
+            pack_words(&d, a->kw, a->pwords, w.data());
+            u32 *tab;
+            CHK(hipMalloc(&tab, w.size() * 4));
+            CHK(hipMemcpy(tab, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+            a->patg = tab;
+            add_shipped_combine(v, "device-table kernel, table resident", a, bytes, bufB, ob);
+            /* the library's per-call ordering steps around that kernel: a
+             * stream wait on the (long complete) upload event before it, a
+             * reader event recorded after it */
+            hipEvent_t *evs = new hipEvent_t[2];
+            CHK(hipEventCreateWithFlags(&evs[0], hipEventDisableTiming));
+            CHK(hipEventCreateWithFlags(&evs[1], hipEventDisableTiming));
+            CHK(hipEventRecord(evs[0], s));
+            CHK(hipStreamSynchronize(s));
+            v.push_back({"resident + wait on a complete event", bytes, [=](hipStream_t st) {
+                             CHK(hipStreamWaitEvent(st, evs[0], 0));
+                             if (launch_combine_k<true, kLdsDmaNT>(st, *a))
+                                 exit(8);
+                         }, bufB, ob});
+            v.push_back({"resident + reader event record", bytes, [=](hipStream_t st) {
+                             if (launch_combine_k<true, kLdsDmaNT>(st, *a))
+                                 exit(8);
+                             CHK(hipEventRecord(evs[1], st));
+                         }, bufB, ob});
+            run_group(title, v, rounds, iters, s);
+            v.clear();
+            return;
+        }
         add_shipped_combine(v, "shipped", a, bytes, bufB, ob);
+        {
+            /* the same patterns read from a device table (the kernel the
+             * library runs past the argument space), table resident */
+            CombineArgs *ap = new CombineArgs(*a);
+            std::vector<u32> w((size_t)a->pwords * a->npatterns, 0u);
+            pack_words(&d, a->kw, a->pwords, w.data());
+            u32 *tab;
+            CHK(hipMalloc(&tab, w.size() * 4));
+            CHK(hipMemcpy(tab, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+            ap->patg = tab;
+            add_shipped_combine(v, "device-table kernel, same patterns", ap, bytes, bufB, ob);
+        }
+        /* controls (r06): the mixed mechanism with every group on pattern 0,
+         * and pattern 0 as a plain single-pattern call */
+        {
+            uint8_t *dz;
+            CHK(hipMalloc(&dz, ngroups));
+            CHK(hipMemset(dz, 0, ngroups));
+            ecd_combine_desc_t dz_d = d;
+            dz_d.group_pattern = dz;
+            CombineArgs *az = new CombineArgs;
+            ecd_combine_desc_t d1 = d;
+            d1.npatterns = 1;
+            d1.group_pattern = nullptr;
+            d1.group_shift = 0;
+            CombineArgs *a1 = new CombineArgs;
+            if (ecdk_pack_args(&dz_d, az) == 0)
+                add_shipped_combine(v, "shipped, map all pattern 0", az, bytes, bufB, ob);
+            if (ecdk_pack_args(&d1, a1) == 0)
+                add_shipped_combine(v, "shipped, pattern 0 single (not mixed)", a1, bytes, bufB, ob);
+        }
         auto addm = [&](const char *nm, auto kern, int nw, size_t lds) {
             lds_attr((const void *)kern, lds);
             const uint64_t g = (nst + 3) / 4;
@@ -1386,6 +1459,17 @@ int main(int argc, char **argv)
         mixed_group(std::integral_constant<int, 8>{}, 12, 16, "mixed 8+4, 16 patterns, 1024-stripe groups");
     if (want(groups, "mixed16"))
         mixed_group(std::integral_constant<int, 16>{}, 20, 7, "mixed 16+4, 7 patterns, 1024-stripe groups");
+    /* r06: disjoint fragments; 64 masks of 16+4 (the bench's configs[4] call,
+     * device pattern table) */
+    if (want(groups, "mixed8s"))
+        mixed_group(std::integral_constant<int, 8>{}, 12, 16, "mixed 8+4, 16 patterns, disjoint fragments",
+                    true);
+    if (want(groups, "mixed16s")) {
+        mixed_group(std::integral_constant<int, 16>{}, 20, 7, "mixed 16+4, 7 patterns, disjoint fragments",
+                    true);
+        mixed_group(std::integral_constant<int, 16>{}, 20, 64,
+                    "mixed 16+4, 64 patterns, disjoint fragments", true);
+    }
     /* LDS-DMA staging policy (r03): the shipped choice by input size against
      * the default and the non-temporal policy at every size, same process;
      * bytes up to the GiB argument */
