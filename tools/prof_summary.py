@@ -10,6 +10,11 @@ For every config directory triple (<cfg>_trace, <cfg>_FETCH_SIZE,
     read, so read bytes = 2 * 1024 * FETCH_SIZE; write bytes = 1024 *
     WRITE_SIZE (exact for 16-B-per-lane stores).
 Algorithmic bytes per launch: encode S*(1+n/k), decode 2*S.
+With tools/profile.sh's WARM_MS (launches keep running that long before the
+40 timed ones), a second duration column averages the last 40 launches of
+the kernel from the kernel trace: the rate past the clock transient of the
+first ~10 ms of load, beside the all-launch average of
+rocprofv3 --stats.
 
 Usage: tools/prof_summary.py gpurun_out/prof_r01 profiles/r01 [traffic.json]
 """
@@ -37,6 +42,22 @@ def stats(d):
             out[s] = dict(calls=int(row["Calls"]), avg_ns=float(row["AverageNs"]),
                           min_ns=float(row["MinNs"]), max_ns=float(row["MaxNs"]))
     return out
+
+
+def tail_avg_ns(d, kern, last=40):
+    """average duration of the kernel's last `last` launches (kernel trace)"""
+    p = os.path.join(d, "run_kernel_trace.csv")
+    if not os.path.exists(p):
+        return None, 0
+    rows = []
+    for r in csv.DictReader(open(p)):
+        if short(r["Kernel_Name"]) == kern:
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    rows.sort()
+    rows = rows[-last:]
+    if not rows:
+        return None, 0
+    return sum(e - b for b, e in rows) / len(rows), len(rows)
 
 
 def counter(d, cname):
@@ -74,9 +95,10 @@ def main():
         gib[name] = float(val)
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     lines = ["# rocprofv3 summary (%s)" % os.path.basename(src.rstrip("/")), "",
-             "| config | kernel | calls | avg us | user GB/s | algorithmic GB/s | HBM frac "
-             "(8 TB/s) | PMC read MB | PMC write MB | PMC/algorithmic |",
-             "|---|---|---|---|---|---|---|---|---|---|"]
+             "| config | kernel | calls | avg us (all) | user GB/s | algorithmic GB/s | HBM frac "
+             "(8 TB/s) | avg us, last 40 | HBM frac, last 40 | PMC read MB | PMC write MB | "
+             "PMC/algorithmic |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|"]
     traffic = {}
     for tdir in sorted(glob.glob(os.path.join(src, "*_trace"))):
         cfg = os.path.basename(tdir)[:-len("_trace")]
@@ -103,10 +125,13 @@ def main():
         rd = fs.get(kern, 0) * 1024 * 2
         wr = ws.get(kern, 0) * 1024
         t = s["avg_ns"] / 1e9
-        lines.append("| %s | `%s` | %d | %.1f | %.0f | %.0f | %.3f | %.1f | %.1f | %.3f |" % (
+        tail, ntail = tail_avg_ns(tdir, kern)
+        tail_cols = ("%.1f | %.3f" % (tail / 1e3, alg / (tail / 1e9) / 8e12)) if tail else "- | -"
+        lines.append("| %s | `%s` | %d | %.1f | %.0f | %.0f | %.3f | %s | %.1f | %.1f | %.3f |" % (
             cfg, kern, s["calls"], s["avg_ns"] / 1e3, S / t / 1e9, alg / t / 1e9,
-            alg / t / 8e12, rd / 1e6, wr / 1e6, (rd + wr) / alg))
-        traffic[cfg] = dict(kernel=kern, avg_ns=s["avg_ns"], user_bytes=S,
+            alg / t / 8e12, tail_cols, rd / 1e6, wr / 1e6, (rd + wr) / alg))
+        traffic[cfg] = dict(kernel=kern, avg_ns=s["avg_ns"], tail_avg_ns=tail, tail_launches=ntail,
+                            user_bytes=S,
                             algorithmic_bytes=alg, hbm_read_bytes=rd, hbm_write_bytes=wr,
                             hbm_bytes_per_launch=rd + wr)
     lines += ["", "PMC correction: read = 2 x 1024 x FETCH_SIZE (gfx950 counts half of a "
