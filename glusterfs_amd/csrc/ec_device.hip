@@ -1240,10 +1240,32 @@ struct EncodeJob {
     bool generic;           /* rows of enc_pat, not the k+n Vandermonde   */
 };
 
+/* A 16+4 host-buffer encode launch of 2048 to 8191 stripes (16 to 64 MiB of
+ * input) runs as a combine with the encode matrix as its pattern (r06): the
+ * double-buffered zero-copy combine stages its inputs in 512-byte pieces
+ * through LDS (1 KiB per wave instruction), where the register-resident
+ * ec_encode_vander_zc<16, 20> reads 64-byte plane segments.  Pinned calls,
+ * same box, alternating (tools/zc_sizes.py, profiles/r06/r06w_zcsizes.log):
+ * 16 MiB 739 -> 596-600 us (+23 %), 64 MiB a tie, 256 / 512 MiB 4 % slower
+ * (the register encoder's 36.4-36.9 GB/s there is the link's write side),
+ * hence the upper bound.  EC_MI355X_ZCENC16=0 keeps the register encoder. */
+constexpr uint64_t kZcEnc16MinStripes = 2048, kZcEnc16MaxStripes = 8192;
+static bool zcenc16_combine()
+{
+    static const bool v = [] {
+        const char *e = getenv("EC_MI355X_ZCENC16");
+        return !(e && *e == '0');
+    }();
+    return v;
+}
+
 int launch_encode(hipStream_t st, const EncodeJob &j, const uint8_t *din, uint8_t *const *outs,
                   uint64_t cnt)
 {
-    if (!j.generic && ecdk_has_vander(j.k, j.n)) /* host buffers: the zero-copy kernel */
+    const bool as_combine = j.generic || !ecdk_has_vander(j.k, j.n) ||
+                            (j.k > 8 && cnt >= kZcEnc16MinStripes && cnt < kZcEnc16MaxStripes &&
+                             j.enc_pat && zcenc16_combine());
+    if (!as_combine)                           /* host buffers: the zero-copy kernel */
         return ecdk_encode_vander(st, j.k, j.n, cnt, din, (void *const *)outs, true);
     ecd_combine_desc_t d;
     memset(&d, 0, offsetof(ecd_combine_desc_t, pat));

@@ -928,6 +928,14 @@ static int cu_count()
     return n;
 }
 
+/* k > 8 with >= 2048 stripes (16 MiB of a 16+4 call): the 4-stripe tiles of
+ * ec_combine_zc_db, two input tiles and the output tile in LDS */
+static bool zc_db4_fits(const ecd_combine_desc_t *d)
+{
+    const size_t lds_db4 = (size_t)(2 * d->k + d->rows) * 4 * ECD_CHUNK + 8 * ECD_MAX_ROWS;
+    return d->k > 8 && d->nstripes >= 2048 && lds_db4 <= (128u << 10) + 8 * ECD_MAX_ROWS;
+}
+
 /* Host-buffer path: every buffer is pinned host memory read / written over
  * PCIe (ec_device.hip run_pipeline), so the zero-copy combine with whole
  * 1 KiB request runs; default (not non-temporal) stores there, which cost
@@ -936,7 +944,10 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
 {
     CombineArgs a;
     int rc = ecdk_pack_args(d, &a);
-    if (rc == -E2BIG || (rc == 0 && (d->k + d->rows > 32 || (d->group_pattern && d->group_shift < 3))))
+    /* more than 32 inputs + rows fit only the 4-stripe double-buffered tile
+     * below (a 16+4 encode as a combine: 16 inputs, 20 rows, r06) */
+    const bool wide = d->k + d->rows > 32 && !(zc_double_buffered() && zc_db4_fits(d));
+    if (rc == -E2BIG || (rc == 0 && (wide || (d->group_pattern && d->group_shift < 3))))
         return combine_any<false>(s, d);   /* device pattern table / LDS limit / small groups */
     if (rc)
         return rc;
@@ -954,8 +965,7 @@ int ecdk_combine_host(hipStream_t s, const ecd_combine_desc_t *d)
      * -> this): 16 MiB 570-576 -> 525 us, 64 MiB 1793-1797 -> 1639; at 4 MiB
      * 172 -> 177, so calls below 2048 stripes (16 MiB) keep ec_combine_zc */
     const size_t lds_db4 = (size_t)(2 * d->k + d->rows) * 4 * ECD_CHUNK + 8 * ECD_MAX_ROWS;
-    const bool db16t4 = d->k > 8 && !db16 && a.nstripes >= 2048 &&
-                        lds_db4 <= (128u << 10) + 8 * ECD_MAX_ROWS;
+    const bool db16t4 = !db16 && zc_db4_fits(d);
     if (zc_double_buffered() && db16t4) {
         const uint64_t g4 = (a.nstripes + 3) / 4;
         const uint64_t tpb = zc_fixed_tpb();

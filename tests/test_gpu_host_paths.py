@@ -205,6 +205,30 @@ def test_decode_16p4_host_kinds(ec, oracle, kind, group):
         p.close()
 
 
+@pytest.mark.parametrize("kind", ["pinned", "pageable"])
+@pytest.mark.parametrize("nst", [2047, 3 * 1024 + 13])
+def test_encode_16p4_host_kinds(ec, oracle, kind, nst):
+    """16+4 encodes of host buffers (r06): from 2048 stripes the encode runs
+    as a combine with the encode matrix as its pattern (20 rows of the
+    4-stripe double-buffered zero-copy kernel), below it the register
+    encoder; every fragment against the oracle, no CPU fallback."""
+    k, n = 16, 20
+    data = rand_bytes(CHUNK * k * nst, seed=nst)
+    want = oracle.encode(k, n, data, nthreads=8)
+    p = Bufs(ec, kind)
+    try:
+        src = p.new(data.size, data)
+        frags = [p.new(CHUNK * nst, 0) for _ in range(n)]
+        s0 = ec.ec_method.stats()
+        with ec.ECMatrixList(k, n) as L:
+            L.encode_batch(nst, src, frags)
+        for i in range(n):
+            assert np.array_equal(frags[i], want[i]), i
+        assert ec.ec_method.stats()["cpu_fallbacks"] == s0["cpu_fallbacks"]
+    finally:
+        p.close()
+
+
 def test_register_overlap_refused(ec):
     """Two registrations must not share a page (the runtime maps pages
     whole; unregistering one would unmap the other's): a range overlapping

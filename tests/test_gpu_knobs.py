@@ -10,7 +10,10 @@ EC_MI355X_ZCDB=0 runs host-buffer combines (k <= 8) through the one tile per
 block zero-copy kernel instead of the persistent double-buffered one (the
 default since r04; =1 forces it), each with host encode, decode, heal and
 mixed calls; EC_ZC_TPB (fixed tiles per block) and EC_ZC_INFLIGHT_KB (input
-bytes in flight per round of tiles) size the persistent zero-copy grid.
+bytes in flight per round of tiles) size the persistent zero-copy grid;
+EC_MI355X_ZCENC16=0 keeps 16+4 host-buffer encodes of >= 2048 stripes on the
+register-resident ec_encode_vander_zc instead of the combine with the encode
+matrix as its pattern (r06).
 (r06 retired the measured-negative knobs EC_MI355X_CHUNK_MB,
 EC_MI355X_TILE_PERM and EC_HELPER_SPIN_US from the product: the XCD tile
 order is now a compile-time choice of the >= 4 GiB 16+4 encoder, covered by
@@ -117,7 +120,7 @@ print("ok")
 
 KNOBS = [("EC_MI355X_ENC", "0"), ("EC_MI355X_PATCACHE", "0"), ("EC_MI355X_LDSNT", "1"),
          ("EC_MI355X_ZCDB", "0"), ("EC_MI355X_ZCDB", "1"), ("EC_ZC_TPB", "1"), ("EC_ZC_TPB", "16"),
-         ("EC_ZC_INFLIGHT_KB", "64")]
+         ("EC_ZC_INFLIGHT_KB", "64"), ("EC_MI355X_ZCENC16", "0")]
 
 
 @pytest.mark.parametrize("knob,value", KNOBS, ids=["%s=%s" % kv for kv in KNOBS])

@@ -28,7 +28,7 @@ def pinned(lib, nb):
 def main():
     lib = g.ec_method.lib
     knobs = " ".join("%s=%s" % (v, os.environ.get(v, "unset"))
-                     for v in ("EC_MI355X_ZCDB", "EC_ZC_TPB", "EC_ZC_INFLIGHT_KB"))
+                     for v in ("EC_MI355X_ZCDB", "EC_ZC_TPB", "EC_ZC_INFLIGHT_KB", "EC_MI355X_ZCENC16"))
     print(knobs)
     sizes = [float(x) for x in os.environ.get("ZC_SIZES", "4 16 64 256").split()]
     geos = [tuple(int(x) for x in gk.split("+")) for gk in
