@@ -601,10 +601,103 @@ __device__ __forceinline__ void stage_tile_shift(uint8_t *lds, const EncSrc src,
     }
 }
 
+/* SM = 8 (r06, kb3 A/B only, measured slower): as SM = 3, but every
+ * 16-byte load at the 16-byte boundary at or below the piece, so a
+ * quarter-wave's 256 bytes never straddle a third 128-byte line; the piece
+ * is funnel-shifted out of the lane's 4 dwords and the next lane's 4 (DPP
+ * row_shl:1 each) by the interior's shift r = 4 dq + sb (uniform: one scalar
+ * switch on dq).  Bit-exact, but 1 / 7 / 16 % slower than SM = 3 for 4+2 /
+ * 8+4 / 16+4 at interior shifts 3, 7 and 13 (profiles/r06/r06zb_kb3_rmw.log):
+ * the 8 staged dwords per piece and 4 DPPs cost more than the straddled
+ * lines, which were not what held the partial writes back. */
+template <int K, int T, int NW>
+__device__ __forceinline__ void stage_tile_shift16(uint8_t *lds, const EncSrc src, uint64_t t0,
+                                                   uint64_t nstripes, u32 wave, u32 lane)
+{
+    constexpr u32 S = K * ECD_CHUNK;
+    constexpr u32 PS = K * 32u;                            /* pieces per stripe */
+    constexpr u32 NP = T * PS;
+    constexpr u32 IT = (NP + NW * 64 - 1) / (NW * 64);
+    const u32 r16 = (u32)(uintptr_t)src.in & 15u;          /* the interior's shift */
+    u32 d[IT][8], dst[IT];
+    bool own[IT], edg[IT];
+#pragma unroll
+    for (u32 it = 0; it < IT; ++it) {
+        const u32 m = it * (NW * 64) + wave * 64 + lane;   /* piece, memory order */
+        const u32 s = m / PS, o = m % PS * 16u;
+        const uint64_t st = t0 + s;
+        dst[it] = ~0u;
+        own[it] = (lane & 15u) == 15u || o + 16u == S;
+        edg[it] = false;
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+            d[it][w] = 0;
+        if (m < NP && st < nstripes) {
+            const u32 p = o / ECD_CHUNK, b = o % ECD_CHUNK / 64u, q = o % 64u / 16u;
+            dst[it] = ((p * 8 + b) * T + s) * 64u + q * 16u;
+            edg[it] = src.edge && (st == 0 || st == nstripes - 1);
+            const uint8_t *a = edg[it] ? src.edge + (st == 0 ? 0u : S) + o : src.in + st * S + o;
+            const u32 r = edg[it] ? 0u : r16;
+            const v4u *al = reinterpret_cast<const v4u *>(__builtin_assume_aligned(a - r, 16));
+            const v4u v = al[0];
+            d[it][0] = v.x;
+            d[it][1] = v.y;
+            d[it][2] = v.z;
+            d[it][3] = v.w;
+            if (r && own[it]) {
+                const v4u e = al[1];            /* holds the last wanted byte */
+                d[it][4] = e.x;
+                d[it][5] = e.y;
+                d[it][6] = e.z;
+                d[it][7] = e.w;
+            }
+        }
+    }
+    const u32 dq = r16 >> 2, sb = r16 & 3u;
+#pragma unroll
+    for (u32 it = 0; it < IT; ++it) {
+        u32 f[8];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            f[w] = d[it][w];
+            const u32 nx = (u32)__builtin_amdgcn_update_dpp(0, (int)d[it][w], 0x101, 0xF, 0xF, false);
+            f[w + 4] = own[it] ? d[it][w + 4] : nx;
+        }
+        if (dst[it] == ~0u)
+            continue;
+        v4u v;
+        if (edg[it] || r16 == 0) {
+            v = v4u{f[0], f[1], f[2], f[3]};
+        } else {
+            switch (dq) {              /* uniform */
+            case 0:
+                v = v4u{__builtin_amdgcn_alignbyte(f[1], f[0], sb), __builtin_amdgcn_alignbyte(f[2], f[1], sb),
+                        __builtin_amdgcn_alignbyte(f[3], f[2], sb), __builtin_amdgcn_alignbyte(f[4], f[3], sb)};
+                break;
+            case 1:
+                v = v4u{__builtin_amdgcn_alignbyte(f[2], f[1], sb), __builtin_amdgcn_alignbyte(f[3], f[2], sb),
+                        __builtin_amdgcn_alignbyte(f[4], f[3], sb), __builtin_amdgcn_alignbyte(f[5], f[4], sb)};
+                break;
+            case 2:
+                v = v4u{__builtin_amdgcn_alignbyte(f[3], f[2], sb), __builtin_amdgcn_alignbyte(f[4], f[3], sb),
+                        __builtin_amdgcn_alignbyte(f[5], f[4], sb), __builtin_amdgcn_alignbyte(f[6], f[5], sb)};
+                break;
+            default:
+                v = v4u{__builtin_amdgcn_alignbyte(f[4], f[3], sb), __builtin_amdgcn_alignbyte(f[5], f[4], sb),
+                        __builtin_amdgcn_alignbyte(f[6], f[5], sb), __builtin_amdgcn_alignbyte(f[7], f[6], sb)};
+                break;
+            }
+        }
+        *reinterpret_cast<v4u *>(lds + dst[it]) = v;
+    }
+}
+
 /* SM (staging mode): 0 = LDS-DMA from in; 1 = LDS-DMA, stripes 0 and
  * nstripes - 1 from edge (partial-stripe writes); 2 = through registers
  * (stage_tile_realign, r03 A/B: slower than LDS-DMA at every alignment);
- * 3 = dword-aligned loads through registers (stage_tile_shift, r05) */
+ * 3 = dword-aligned loads through registers (stage_tile_shift, r05);
+ * 8 = 16-byte-aligned loads through registers (stage_tile_shift16, r06;
+ * kb3 A/B, slower) */
 template <int K, int T, int NW, int SM, int LA = kLdsDmaDefault>
 __device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src, uint64_t t0,
                                                   uint64_t nstripes, u32 wave, u32 lane)
@@ -614,6 +707,8 @@ __device__ __forceinline__ void stage_encode_tile(uint8_t *lds, const EncSrc src
         stage_tile_realign<K, T, NW>(lds, src, t0, nstripes, wave, lane);
     } else if constexpr (SM == 3) {
         stage_tile_shift<K, T, NW>(lds, src, t0, nstripes, wave, lane);
+    } else if constexpr (SM == 8) {
+        stage_tile_shift16<K, T, NW>(lds, src, t0, nstripes, wave, lane);
     } else if constexpr (SM == 7) {
         /* kb3 A/B: shift staging with non-temporal loads */
         stage_tile_shift<K, T, NW, 0, true>(lds, src, t0, nstripes, wave, lane);

@@ -859,6 +859,22 @@ int main(int argc, char **argv)
                              hipLaunchKernelGGL(kern3, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
                                                 EncSrc{ushift, edge}, f, nst);
                          }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            auto kern8 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 8>;
+            v.push_back({"16-byte-aligned shift staging (SM=8)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern8, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            for (u32 sh : {7u, 13u}) {   /* dword shifts 1 and 3 (timing only) */
+                const uint8_t *us = bufA + sh;
+                v.push_back({std::string("SM=3 at +") + std::to_string(sh), bytes, [=](hipStream_t st) {
+                                 hipLaunchKernelGGL(kern3, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                    EncSrc{us, edge}, f, nst);
+                             }, nullptr, 0});
+                v.push_back({std::string("SM=8 at +") + std::to_string(sh), bytes, [=](hipStream_t st) {
+                                 hipLaunchKernelGGL(kern8, dim3((u32)((nst + 3) / 4)), dim3(640), lds, st,
+                                                    EncSrc{us, edge}, f, nst);
+                             }, nullptr, 0});
+            }
             auto kern4 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 4>;
             auto kern5 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 5>;
             auto kern6 = ec_encode_tile_rb<16, 20, 4, 2, true, true, 6>;
@@ -892,6 +908,22 @@ int main(int argc, char **argv)
                              hipLaunchKernelGGL(kern3, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
                                                 EncSrc{ushift, edge}, f, nst);
                          }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            auto kern8 = ec_encode_tile_t<K, N, 4, NW, true, (K == 4), true, 8>;
+            v.push_back({"16-byte-aligned shift staging (SM=8)", bytes, [=](hipStream_t st) {
+                             hipLaunchKernelGGL(kern8, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
+                                                EncSrc{ushift, edge}, f, nst);
+                         }, f.p[N - 1], (size_t)nst * ECD_CHUNK});
+            for (u32 sh : {7u, 13u}) {   /* dword shifts 1 and 3 (timing only) */
+                const uint8_t *us = bufA + sh;
+                v.push_back({std::string("SM=3 at +") + std::to_string(sh), bytes, [=](hipStream_t st) {
+                                 hipLaunchKernelGGL(kern3, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
+                                                    EncSrc{us, edge}, f, nst);
+                             }, nullptr, 0});
+                v.push_back({std::string("SM=8 at +") + std::to_string(sh), bytes, [=](hipStream_t st) {
+                                 hipLaunchKernelGGL(kern8, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
+                                                    EncSrc{us, edge}, f, nst);
+                             }, nullptr, 0});
+            }
             auto kern7 = ec_encode_tile_t<K, N, 4, NW, true, (K == 4), true, 7>;
             v.push_back({"shift staging, non-temporal loads (SM=7)", bytes, [=](hipStream_t st) {
                              hipLaunchKernelGGL(kern7, dim3((u32)((nst + 3) / 4)), dim3(64 * NW), lds, st,
